@@ -1,0 +1,145 @@
+/* ccdgpu.h -- C-ABI of libccdgpu.so: MI355X (gfx950) CCDC change detection.
+ *
+ * Drop-in replacement for the per-pixel call the reference makes at
+ *     ccdc/pyccd.py:168   ccdresult = ccd.detect(**second(timeseries))
+ * (lcmap-pyccd 2018.03.12.dev-ncompare.b2, setup.py:32) over the records that
+ *     ccdc/timeseries.py:92-126   (merlin.create -> ((cx,cy,px,py), {dates, blues..thermals, qas}))
+ * builds.  One call processes a batch of pixels that share one acquisition-date vector (a chip
+ * or part of one, as merlin builds them per chip).  The Python side (lcmap-firebird_amd/ccd,
+ * lcmap-firebird_amd/ccdc/pyccd.py) binds these symbols with ctypes; INTEGRATION.md shows the
+ * binding.  Plain C types only; no C++ or torch types cross this boundary.
+ *
+ * Errors: every entry point returns 0 on success or a negative CCDGPU_E* code; the message of the
+ * last failure on the calling thread is ccdgpu_last_error().  An unsupported bit-packed QA value
+ * is CCDGPU_EQA -- the analogue of pyccd's ValueError from qa.qabitval -- and the offending
+ * pixel is reported in ccdgpu_result.error_pixel.
+ */
+#ifndef CCDGPU_H
+#define CCDGPU_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CCDGPU_OK 0
+#define CCDGPU_EINVAL (-1)   /* bad argument / size                                    */
+#define CCDGPU_EHIP (-2)     /* HIP runtime error (no device, launch failure, ...)     */
+#define CCDGPU_EQA (-3)      /* unsupported bit-packed QA value (pyccd ValueError)     */
+#define CCDGPU_ENOMEM (-4)   /* device or host allocation failed                       */
+#define CCDGPU_EOVERFLOW (-5)/* internal capacity exceeded (segments per pixel, peek)  */
+
+#define CCDGPU_NBANDS 7      /* blue, green, red, nir, swir1, swir2, thermal            */
+#define CCDGPU_MAX_OBS 4096  /* observations per pixel the kernels accept              */
+#define CCDGPU_MAX_PEEK 64   /* largest (adaptive) look-ahead window                     */
+
+/* ccd/parameters.yaml defaults; ccdgpu_params_default() fills them. */
+typedef struct ccdgpu_params {
+    int32_t meow_size;          /* 12   MEOW_SIZE                                       */
+    int32_t peek_size;          /* 6    PEEK_SIZE (default; ncompare may enlarge it)     */
+    int32_t day_delta;          /* 365  DAY_DELTA                                        */
+    int32_t coef_min, coef_mid, coef_max; /* 4 / 6 / 8                                    */
+    int32_t num_obs_factor;     /* 3                                                     */
+    uint32_t detection_bands;   /* bit mask, default bands 1..5 = 0x3E                   */
+    uint32_t tmask_bands;       /* bit mask, default bands 1 and 4 = 0x12                */
+    int32_t lasso_max_iter;     /* 1000                                                  */
+    int32_t thermal_min, thermal_max; /* -9320 / 7070 (deg C x 100)                        */
+    int32_t median_green_filter;/* 400                                                   */
+    int32_t curve_qa_start, curve_qa_end, curve_qa_insuf_clear, curve_qa_persist_snow; /* 14/24/44/54 */
+    int32_t qa_fill, qa_clear, qa_water, qa_shadow, qa_snow, qa_cloud; /* bit offsets 0..5 */
+    int32_t qa_cirrus1, qa_cirrus2, qa_occlusion;                      /* 8, 9, 10         */
+    int32_t qa_bitpacked;       /* 1: qas are PIXELQA bit fields; 0: already class ids   */
+    int32_t adaptive_peek;      /* 1: "ncompare" density-adaptive peek + threshold        */
+    int32_t rmse_dof;           /* 1: rmse denominator n - num_coefficients              */
+    int32_t kelvin_to_celsius;  /* 1: standard procedure converts thermal (int16 wrap)   */
+    double avg_days_yr;         /* 365.2425                                              */
+    double change_probability;  /* 0.99                                                  */
+    double change_threshold;    /* chi2.ppf(0.99, 5)                                     */
+    double outlier_threshold;   /* chi2.ppf(0.999999, 5)                                 */
+    double t_const;             /* 4.42 Tmask                                            */
+    double lasso_alpha;         /* 1.0 (sklearn Lasso alpha; l1 = alpha * n_samples)     */
+    double lasso_tol;           /* 1e-4                                                  */
+    double clear_pct_threshold; /* 0.25                                                  */
+    double snow_pct_threshold;  /* 0.75                                                  */
+} ccdgpu_params;
+
+/* One change model (pyccd change_model dict; ccdc/pyccd.py:106-148 formats it). */
+typedef struct ccdgpu_segment {
+    int32_t start_day, end_day, break_day; /* proleptic ordinals                       */
+    int32_t observation_count;
+    int32_t curve_qa;
+    int32_t pixel;                          /* pixel index within the batch             */
+    double change_probability;
+    double magnitude[CCDGPU_NBANDS];
+    double rmse[CCDGPU_NBANDS];
+    double intercept[CCDGPU_NBANDS];
+    double coef[CCDGPU_NBANDS][7];          /* [band][t, cos, sin, cos2, sin2, cos3, sin3] */
+} ccdgpu_segment;
+
+enum { CCDGPU_PROC_STANDARD = 0, CCDGPU_PROC_PERMANENT_SNOW = 1, CCDGPU_PROC_INSUFFICIENT_CLEAR = 2 };
+
+/* Results, CSR by pixel.  Owned by the library until ccdgpu_result_free. */
+typedef struct ccdgpu_result {
+    int32_t n_pix, n_obs;
+    int64_t n_seg;
+    int64_t *seg_offsets;       /* [n_pix + 1]                                            */
+    ccdgpu_segment *segments;   /* [n_seg], pixel-major, in detection order               */
+    uint32_t *mask_bits;        /* [n_pix][mask_words] processing_mask, SORTED date order  */
+    int32_t mask_words;         /* (n_obs + 31) / 32                                      */
+    int32_t *procedure;         /* [n_pix] CCDGPU_PROC_*                                  */
+    double *probs;              /* [n_pix][3] cloud, snow, water                          */
+    int64_t *sorted_dates;      /* [n_obs] ascending (stable argsort of the input dates)  */
+    int32_t *sort_index;        /* [n_obs] input position of each sorted observation      */
+    int32_t error_pixel;        /* first pixel with an unsupported QA value, else -1      */
+    double seconds_kernel;      /* device time of the detection kernels (HIP events)      */
+    double seconds_total;       /* wall time of the call                                  */
+} ccdgpu_result;
+
+typedef struct ccdgpu_ctx ccdgpu_ctx;
+
+const char *ccdgpu_version(void);
+const char *ccdgpu_last_error(void);
+void ccdgpu_params_default(ccdgpu_params *p);
+
+/* Create a context bound to HIP device `device` (one context per device and host thread). */
+int ccdgpu_init(int device, ccdgpu_ctx **ctx);
+int ccdgpu_destroy(ccdgpu_ctx *ctx);
+int ccdgpu_device_count(int *count);
+int ccdgpu_synchronize(ccdgpu_ctx *ctx);
+
+/* Host-buffer entry point (the pyccd.detect / ccd.detect path).
+ *   dates   [n_obs]                 ordinals, any order (merlin delivers them descending)
+ *   spectra [7][n_pix][n_obs]       int16, band-major, observation-contiguous, input order
+ *   qa      [n_pix][n_obs]          uint16 bit-packed PIXELQA (or class ids if !qa_bitpacked)
+ * Synchronous: H2D, kernels, D2H.  *out must be released with ccdgpu_result_free. */
+int ccdgpu_detect_batch(ccdgpu_ctx *ctx, const ccdgpu_params *params, int32_t n_pix, int32_t n_obs,
+                        const int64_t *dates, const int16_t *spectra, const uint16_t *qa,
+                        ccdgpu_result *out);
+void ccdgpu_result_free(ccdgpu_result *out);
+
+/* Device-resident path (benchmarks, multi-chip pipelines): stage a batch once, run the
+ * detection as often as wanted on the resident copy, fetch results separately.  Up to
+ * `n_chips` chips of identical (n_pix, n_obs) shape are staged back to back; chip c's arrays
+ * start at c * n_obs / c * 7 * n_pix * n_obs / c * n_pix * n_obs elements of the host buffers. */
+int ccdgpu_stage(ccdgpu_ctx *ctx, const ccdgpu_params *params, int32_t n_chips, int32_t n_pix,
+                 int32_t n_obs, const int64_t *dates, const int16_t *spectra, const uint16_t *qa);
+int ccdgpu_run_staged(ccdgpu_ctx *ctx, double *kernel_seconds);
+int ccdgpu_fetch_staged(ccdgpu_ctx *ctx, int32_t chip, ccdgpu_result *out);
+
+/* Kernel statistics of the last run (per launch of the main detection kernel). */
+typedef struct ccdgpu_stats {
+    double detect_ms;           /* average duration of the detection kernel (HIP events)   */
+    double prep_ms;             /* average duration of the per-chip preparation kernel     */
+    int64_t pixels;             /* pixels processed by the last run                        */
+    int64_t segments;           /* segments written                                        */
+    int64_t lasso_fits;         /* band-model fits (7 per model)                           */
+    int64_t cd_sweeps;          /* coordinate-descent sweeps summed over fits              */
+    int64_t flops;              /* counted FP64 flops (SURVEY.md §8(d) op-count model)     */
+    int64_t bytes;              /* algorithmic HBM bytes read+written                      */
+} ccdgpu_stats;
+int ccdgpu_last_stats(ccdgpu_ctx *ctx, ccdgpu_stats *stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

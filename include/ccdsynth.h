@@ -1,0 +1,44 @@
+/* ccdsynth.h -- deterministic synthetic Landsat ARD chip generator (bench / test input only).
+ *
+ * Produces the per-chip record layout that ccdc/timeseries.py:92-126 builds through
+ * merlin.create (dates descending as merlin delivers them, timeseries.py:115; int16 spectra
+ * with fill -9999; uint16 bit-packed PIXELQA), in the band-major, observation-contiguous layout
+ * the detection ABI consumes (include/ccdgpu.h).  Configs follow SURVEY.md §8(d): C2 (chip,
+ * n~1000), C3 (tile cadence L4-L8 1982-2017 + sidelap), C4 (high cloud/snow), C5 (breaks every
+ * ~3 yr).  Counter-based RNG: every value depends only on (seed, chip, pixel, obs), so any subset
+ * of pixels regenerates bit-identically on any host.
+ */
+#ifndef CCDSYNTH_H
+#define CCDSYNTH_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ccdsynth_cfg {
+    int32_t n_obs_target;      /* subsample the cadence down to this many dates (0 = natural) */
+    int32_t sidelap;           /* 1: add the +7 day sidelap path (50 % of its acquisitions)   */
+    int32_t change_every_days; /* 0: no abrupt change; else mean days between breaks          */
+    int32_t first_year_l4;     /* 1: include Landsat 4 (1982-1993)                             */
+    double p_clear, p_cloud, p_shadow, p_snow, p_water, p_fill; /* per-observation class mix  */
+    double p_saturated;        /* share of clear obs with one optical band saturated          */
+    double p_hot_thermal;      /* share of clear obs with thermal > 327.6 K (int16 wrap path)  */
+    uint64_t seed;
+} ccdsynth_cfg;
+
+/* Fill cfg with a named config: 2 = C2 chip, 3 = C3 tile chip, 4 = C4 stress, 5 = C5 change-dense. */
+int ccdsynth_config(int which, ccdsynth_cfg *cfg);
+
+/* Acquisition dates of chip `chip_index` (proleptic Gregorian ordinals, DESCENDING).
+ * Writes at most `cap` values; returns the count (or the required count if dates == NULL). */
+int ccdsynth_dates(const ccdsynth_cfg *cfg, int32_t chip_index, int64_t *dates, int32_t cap);
+
+/* Spectra [7][n_pix][n_obs] (blue, green, red, nir, swir1, swir2, thermal K*10) and
+ * qa [n_pix][n_obs] for pixels pix0 .. pix0+n_pix-1 of the chip (pixel = row*100 + col). */
+int ccdsynth_chip(const ccdsynth_cfg *cfg, int32_t chip_index, int32_t pix0, int32_t n_pix,
+                  int32_t n_obs, const int64_t *dates, int16_t *spectra, uint16_t *qa);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,744 @@
+"""ccd_ref -- numpy restatement of lcmap-pyccd's ``ccd.detect`` (TEST INFRASTRUCTURE ONLY).
+
+THIS MODULE IS AN ORACLE.  Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may import it, and only as the checker.  The product path
+(``lcmap-firebird_amd``) never imports anything under ``oracle/``.
+
+What it restates
+----------------
+The reference (USGS-EROS/lcmap-firebird, ``ccdc/pyccd.py:168``) calls ``ccd.detect(**record)``
+from the *external, un-vendored* package ``lcmap-pyccd==2018.03.12.dev-ncompare.b2``
+(``setup.py:32``; ``requirements-dev.txt:1`` pins commit e1640f7096eb98b0a2530d91a103a949db6672c5)
+which in turn uses scikit-learn 0.18 (``Dockerfile:4``) for its Lasso.  That package is absent
+from this container and cannot be fetched (no network), so this file restates pyccd's published
+algorithm module by module (names below are pyccd's: ``ccd/__init__.py``, ``ccd/qa.py``,
+``ccd/procedures.py``, ``ccd/change.py``, ``ccd/math_utils.py``, ``ccd/models/lasso.py``,
+``ccd/models/tmask.py``, ``ccd/models/robust_fit.py``, ``ccd/parameters.yaml``).  The Lasso is a
+literal numpy port of scikit-learn 0.18's ``cd_fast.enet_coordinate_descent`` (residual-update
+cyclic coordinate descent with the duality-gap stop) applied to the centred design, exactly as
+``sklearn.linear_model.Lasso(max_iter=1000).fit`` does (alpha=1 -> l1_reg = n_samples).
+
+PARITY STATUS: the restatement is pinned by the reference's own boundary tests
+(``test/test_pyccd.py:33-35,37-126,129-132``: default rows, format golden, the all-fill
+4-observation detect) and by ``tests/test_oracle_sklearn.py`` (the Lasso sub-kernel against the
+installed scikit-learn).  The multi-segment numeric behaviour is **parity unpinned** against
+pyccd itself: no fixture in the reference holds a pyccd change-model result.
+Every spec choice that could not be verified against the pinned pyccd source is a named
+parameter (``DEFAULTS`` below) so the GPU path and both oracles can be re-pinned by flipping it.
+
+Deliberate, documented deviations from the numpy reference (both are numpy-build dependent in
+pyccd, so no single "reference" answer exists):
+* ``argsort`` of dates and of closest-day-of-year distances uses a *stable* sort (ties by index);
+  numpy's default quicksort/x86-simd-sort breaks ties differently across builds.
+* a Tmask window spanning exactly 365 days gives a rank-deficient 5-column design (the 1/N-year
+  harmonic equals the annual one); pyccd's QR leverage is then rounding noise.  Here the
+  duplicated columns are dropped (the projection, hence every prediction, is unchanged).
+"""
+
+import math
+
+import numpy as np
+
+try:  # scipy is only needed for the ncompare (adaptive peek) change threshold.
+    from scipy.stats import chi2 as _chi2
+except Exception:  # pragma: no cover
+    _chi2 = None
+
+ALGORITHM = 'lcmap-pyccd:2018.03.12.dev-ncompare.b2'
+
+# ccd/parameters.yaml [ext] -- values as restated in SURVEY.md Appendix A.1.
+DEFAULTS = dict(
+    QA_BITPACKED=True,
+    QA_FILL=0, QA_CLEAR=1, QA_WATER=2, QA_SHADOW=3, QA_SNOW=4, QA_CLOUD=5,
+    QA_CIRRUS1=8, QA_CIRRUS2=9, QA_OCCLUSION=10,
+    CLEAR_PCT_THRESHOLD=0.25,
+    SNOW_PCT_THRESHOLD=0.75,
+    THERMAL_IDX=6,
+    THERMAL_MIN=-9320,           # degrees C x 100 (filter_thermal_celsius)
+    THERMAL_MAX=7070,
+    GREEN_IDX=1,
+    MEDIAN_GREEN_FILTER=400,
+    MEOW_SIZE=12,
+    PEEK_SIZE=6,
+    DAY_DELTA=365,
+    AVG_DAYS_YR=365.2425,
+    COEFFICIENT_MIN=4, COEFFICIENT_MID=6, COEFFICIENT_MAX=8,
+    NUM_OBS_FACTOR=3,
+    DETECTION_BANDS=(1, 2, 3, 4, 5),
+    TMASK_BANDS=(1, 4),
+    CHANGE_PROBABILITY=0.99,
+    CHANGE_THRESHOLD=15.086272469388987,    # chi2.ppf(0.99, 5)
+    OUTLIER_THRESHOLD=35.888186879610423,   # chi2.ppf(0.999999, 5)
+    T_CONST=4.42,
+    LASSO_MAX_ITER=1000,
+    LASSO_ALPHA=1.0,
+    LASSO_TOL=1e-4,
+    CURVE_QA=dict(PERSIST_SNOW=54, INSUF_CLEAR=44, START=14, END=24),
+    # ---- switches for the points SURVEY.md flags as unverifiable ----
+    ADAPTIVE_PEEK=True,      # "ncompare": peek/threshold adapt to observation density (A.6)
+    RMSE_DOF=False,          # rmse denominator n (False) or n - num_coefficients (True)
+    KELVIN_TO_CELSIUS=True,  # standard procedure converts thermal K*10 -> C*100 (int16 wrap)
+)
+
+BANDS = ('blue', 'green', 'red', 'nir', 'swir1', 'swir2', 'thermal')
+
+
+class Params(dict):
+    """ccd/app.py Parameters: attribute access over a fresh dict per detect call."""
+
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError as e:  # pragma: no cover
+            raise AttributeError(k) from e
+
+    def __setattr__(self, k, v):
+        self[k] = v
+
+
+def get_params(params=None):
+    p = Params({k: (dict(v) if isinstance(v, dict) else v) for k, v in DEFAULTS.items()})
+    if params:
+        p.update(params)
+    return p
+
+
+# --------------------------------------------------------------------------- qa.py [ext]
+def checkbit(packedint, offset):
+    return (int(packedint) & (1 << offset)) > 0
+
+
+def qabitval(packedint, p):
+    """qa.qabitval: hierarchy fill > cloud > shadow > snow > water > clear."""
+    if checkbit(packedint, p.QA_FILL):
+        return p.QA_FILL
+    elif checkbit(packedint, p.QA_CLOUD):
+        return p.QA_CLOUD
+    elif checkbit(packedint, p.QA_SHADOW):
+        return p.QA_SHADOW
+    elif checkbit(packedint, p.QA_SNOW):
+        return p.QA_SNOW
+    elif checkbit(packedint, p.QA_WATER):
+        return p.QA_WATER
+    elif checkbit(packedint, p.QA_CLEAR):
+        return p.QA_CLEAR
+    elif checkbit(packedint, p.QA_CIRRUS1) & checkbit(packedint, p.QA_CIRRUS2):
+        return p.QA_CLEAR
+    elif checkbit(packedint, p.QA_OCCLUSION):
+        return p.QA_CLEAR
+    raise ValueError('Unsupported bitpacked QA value {}'.format(packedint))
+
+
+def unpackqa(quality, p):
+    out = np.zeros(quality.shape, dtype=np.int64)
+    for i in range(len(quality)):
+        out[i] = qabitval(quality[i], p)
+    return out
+
+
+def count_value(q, v):
+    return int(np.sum(q == v))
+
+
+def count_total(q, p):
+    return int(np.sum(q != p.QA_FILL))
+
+
+def count_clear_or_water(q, p):
+    return count_value(q, p.QA_CLEAR) + count_value(q, p.QA_WATER)
+
+
+def _div(a, b):
+    # numpy-scalar division semantics (0/0 -> nan, x/0 -> inf) without warnings
+    with np.errstate(divide='ignore', invalid='ignore'):
+        return float(np.float64(a) / np.float64(b))
+
+
+def quality_probabilities(q, p):
+    """qa.quality_probabilities -> (cloud, snow, water).  Not consumed by ccdc.pyccd.format."""
+    snow = count_value(q, p.QA_SNOW)
+    clear = count_clear_or_water(q, p)
+    water = count_value(q, p.QA_WATER)
+    cloud = count_value(q, p.QA_CLOUD)
+    total = count_total(q, p)
+    return (_div(cloud, total),
+            _div(snow, clear + snow + 0.01),
+            _div(water, clear + snow + 0.01))
+
+
+def enough_clear(q, p):
+    return _div(count_clear_or_water(q, p), count_total(q, p)) >= p.CLEAR_PCT_THRESHOLD
+
+
+def enough_snow(q, p):
+    snow = count_value(q, p.QA_SNOW)
+    return _div(snow, count_clear_or_water(q, p) + snow + 0.01) >= p.SNOW_PCT_THRESHOLD
+
+
+def filter_saturated(obs):
+    """qa.filter_saturated: all six optical bands in (0, 10000)."""
+    m = np.ones(obs.shape[1], dtype=bool)
+    for b in range(6):
+        m &= (obs[b] > 0) & (obs[b] < 10000)
+    return m
+
+
+def filter_thermal_celsius(thermal, p):
+    return (thermal > p.THERMAL_MIN) & (thermal < p.THERMAL_MAX)
+
+
+def mask_duplicate_values(vector):
+    """math_utils.mask_duplicate_values: keep the first of each repeated value."""
+    mask = np.zeros(vector.shape, dtype=bool)
+    mask[np.unique(vector, return_index=True)[1]] = True
+    return mask
+
+
+def standard_procedure_filter(obs, q, dates, p):
+    mask = (((q == p.QA_WATER) | (q == p.QA_CLEAR))
+            & filter_thermal_celsius(obs[p.THERMAL_IDX], p)
+            & filter_saturated(obs))
+    mask[mask] = mask_duplicate_values(dates[mask])
+    return mask
+
+
+def snow_procedure_filter(obs, q, dates, p):
+    mask = ((((q == p.QA_WATER) | (q == p.QA_CLEAR))
+             & filter_thermal_celsius(obs[p.THERMAL_IDX], p)
+             & filter_saturated(obs))
+            | (q == p.QA_SNOW))
+    mask[mask] = mask_duplicate_values(dates[mask])
+    return mask
+
+
+def insufficient_clear_filter(obs, q, dates, p):
+    mask = standard_procedure_filter(obs, q, dates, p)
+    sub = obs[:, mask]
+    if sub.shape[1] == 0:
+        return mask
+    med = np.median(sub[p.GREEN_IDX]) + p.MEDIAN_GREEN_FILTER
+    mask[mask] = sub[p.GREEN_IDX] < med
+    return mask
+
+
+# --------------------------------------------------------------------------- math_utils.py [ext]
+def kelvin_to_celsius(thermals, scale=10):
+    """thermals * 10 - 27315 evaluated in the array's dtype (int16 wraps, as numpy does)."""
+    t = thermals.astype(np.int64) * scale - 27315
+    return t.astype(thermals.dtype)
+
+
+def euclidean_norm(v):
+    v = np.asarray(v, dtype=np.float64)
+    return math.sqrt(float(np.sum(v * v)))
+
+
+def calc_rmse(actual, predicted, num_pm=0):
+    residuals = actual - predicted
+    return math.sqrt(float(np.sum(residuals * residuals)) / (len(residuals) - num_pm)), residuals
+
+
+def adjusted_variogram(dates, obs):
+    """math_utils.adjusted_variogram: median |diff| at the first lag whose gaps are mostly >30 d."""
+    if obs.shape[1] < 2:
+        return np.full(obs.shape[0], np.nan)
+    o = obs.astype(np.int64)
+    vario = np.median(np.abs(np.diff(o, axis=1)), axis=1)
+    for idx in range(dates.shape[0] - 1):
+        var = dates[1 + idx:] - dates[:-idx - 1]
+        majority = np.mean(var > 30)
+        if majority >= 0.5:
+            diff = o[:, 1 + idx:] - o[:, :-idx - 1]
+            ids = var > 30
+            vario = np.median(np.abs(diff[:, ids]), axis=1)
+            break
+    return vario.astype(np.float64)
+
+
+# --------------------------------------------------------------------------- models/lasso.py [ext]
+def coefficient_matrix(dates, avg_days_yr, num_coefficients):
+    w = 2 * np.pi / avg_days_yr
+    m = np.zeros((len(dates), 7), order='F')
+    w12 = w * np.asarray(dates, dtype=np.float64)
+    m[:, 0] = dates
+    m[:, 1] = np.cos(w12)
+    m[:, 2] = np.sin(w12)
+    if num_coefficients >= 6:
+        w34 = 2 * w12
+        m[:, 3] = np.cos(w34)
+        m[:, 4] = np.sin(w34)
+    if num_coefficients >= 8:
+        w56 = 3 * w12
+        m[:, 5] = np.cos(w56)
+        m[:, 6] = np.sin(w56)
+    return m
+
+
+def enet_coordinate_descent(X, y, alpha, max_iter, tol):
+    """Port of scikit-learn 0.18 sklearn/linear_model/cd_fast.pyx::enet_coordinate_descent
+    (beta = 0, positive = False, cyclic).  X, y already centred.  Returns (w, n_iter)."""
+    n, p = X.shape
+    w = np.zeros(p)
+    norm_cols = (X ** 2).sum(axis=0)
+    R = y.copy()
+    d_w_tol = tol
+    tol = tol * float(np.dot(y, y))
+    n_iter = 0
+    for n_iter in range(max_iter):
+        w_max = 0.0
+        d_w_max = 0.0
+        for ii in range(p):
+            if norm_cols[ii] == 0.0:
+                continue
+            w_ii = w[ii]
+            if w_ii != 0.0:
+                R += w_ii * X[:, ii]
+            tmp = float(np.dot(X[:, ii], R))
+            w[ii] = math.copysign(max(abs(tmp) - alpha, 0.0), tmp) / norm_cols[ii] if tmp != 0 else 0.0
+            if w[ii] != 0.0:
+                R -= w[ii] * X[:, ii]
+            d_w_ii = abs(w[ii] - w_ii)
+            if d_w_ii > d_w_max:
+                d_w_max = d_w_ii
+            if abs(w[ii]) > w_max:
+                w_max = abs(w[ii])
+        if w_max == 0.0 or d_w_max / w_max < d_w_tol or n_iter == max_iter - 1:
+            XtA = X.T @ R
+            dual_norm_XtA = float(np.max(np.abs(XtA))) if p else 0.0
+            R_norm2 = float(np.dot(R, R))
+            if dual_norm_XtA > alpha:
+                const = alpha / dual_norm_XtA
+                A_norm2 = R_norm2 * const ** 2
+                gap = 0.5 * (R_norm2 + A_norm2)
+            else:
+                const = 1.0
+                gap = R_norm2
+            gap += alpha * float(np.sum(np.abs(w))) - const * float(np.dot(R, y))
+            if gap < tol:
+                break
+    return w, n_iter + 1
+
+
+class FittedModel(object):
+    __slots__ = ('coef', 'intercept', 'rmse', 'residual', 'n_iter')
+
+    def __init__(self, coef, intercept, rmse, residual, n_iter):
+        self.coef, self.intercept, self.rmse, self.residual, self.n_iter = (
+            coef, intercept, rmse, residual, n_iter)
+
+
+def fitted_model(dates, spectra_obs, p, num_coefficients):
+    """models/lasso.fitted_model: Lasso(max_iter).fit(coefficient_matrix, obs), rmse, residuals."""
+    X = coefficient_matrix(dates, p.AVG_DAYS_YR, num_coefficients)
+    y = np.asarray(spectra_obs, dtype=np.float64)
+    n = X.shape[0]
+    X_offset = X.mean(axis=0)
+    y_offset = y.mean()
+    Xc = np.asfortranarray(X - X_offset)
+    yc = y - y_offset
+    w, n_iter = enet_coordinate_descent(Xc, yc, p.LASSO_ALPHA * n, p.LASSO_MAX_ITER, p.LASSO_TOL)
+    intercept = y_offset - float(np.dot(X_offset, w))
+    pred = X @ w + intercept
+    rmse, resid = calc_rmse(y, pred, num_coefficients if p.RMSE_DOF else 0)
+    return FittedModel(w, intercept, rmse, resid, n_iter)
+
+
+def predict(model, dates, p):
+    X = coefficient_matrix(dates, p.AVG_DAYS_YR, 8)
+    return X @ model.coef + model.intercept
+
+
+# --------------------------------------------------------------------------- models/robust_fit.py [ext]
+EPS = np.finfo('float').eps
+
+
+def bisquare(resid, c=4.685):
+    return (np.abs(resid) < c) * (1 - (resid / c) ** 2) ** 2
+
+
+def mad(x, c=0.6745):
+    rs = np.sort(np.abs(x))
+    return np.median(rs[4:]) / c
+
+
+def _check_converge(x0, x, tol=1e-8):
+    # upstream quirk kept: fabs() wraps the boolean (x0 - x > tol)
+    return not np.any(np.fabs(x0 - x > tol))
+
+
+def _weight_fit(X, y, w):
+    sw = np.sqrt(w)
+    Xw = X * sw[:, None]
+    yw = y * sw
+    beta = np.linalg.lstsq(Xw, yw, rcond=None)[0]
+    resid = y - np.dot(X, beta)
+    return beta, resid
+
+
+def rlm_fit(X, y, maxiter=5, tune=4.685, tol=1e-8):
+    """robust_fit.RLM(maxiter=5).fit: bisquare IRLS with QR leverage adjustment."""
+    y = np.asarray(y, dtype=np.float64)
+    coef, resid = _weight_fit(X, y, np.ones_like(y))
+    _, R = np.linalg.qr(X)
+    E = X.dot(np.linalg.inv(R[0:X.shape[1], 0:X.shape[1]]))
+    h = np.minimum(np.ones(X.shape[0]) * 0.9999, np.sum(E * E, axis=1))
+    adjfactor = np.divide(1, np.sqrt(1 - h))
+    iteration = 1
+    converged = 0
+    while not converged and iteration < maxiter:
+        _coef = coef.copy()
+        resid = y - X.dot(_coef)
+        resid = resid * adjfactor
+        scale = max(EPS * np.std(y), mad(resid))
+        weights = bisquare(resid / scale, c=tune)
+        coef, resid = _weight_fit(X, y, weights)
+        iteration += 1
+        converged = _check_converge(coef, _coef, tol=tol)
+    return coef
+
+
+# --------------------------------------------------------------------------- models/tmask.py [ext]
+def tmask_coefficient_matrix(dates, avg_days_yr):
+    annual_cycle = 2 * np.pi / avg_days_yr
+    observation_cycle = annual_cycle / np.ceil((dates[-1] - dates[0]) / avg_days_yr)
+    d = np.asarray(dates, dtype=np.float64)
+    matrix = np.ones((dates.shape[0], 5), order='F')
+    matrix[:, 0] = np.cos(annual_cycle * d)
+    matrix[:, 1] = np.sin(annual_cycle * d)
+    matrix[:, 2] = np.cos(observation_cycle * d)
+    matrix[:, 3] = np.sin(observation_cycle * d)
+    if observation_cycle == annual_cycle:
+        matrix = np.asfortranarray(matrix[:, [0, 1, 4]])  # documented rank-deficiency deviation
+    return matrix
+
+
+def tmask(dates, obs, variogram, p):
+    X = tmask_coefficient_matrix(dates, p.AVG_DAYS_YR)
+    outliers = np.zeros(obs.shape[1], dtype=bool)
+    for b in p.TMASK_BANDS:
+        coef = rlm_fit(X, obs[b])
+        predicted = np.dot(X, coef) + 0.0
+        outliers |= np.abs(predicted - obs[b]) > variogram[b] * p.T_CONST
+    return outliers
+
+
+# --------------------------------------------------------------------------- change.py [ext]
+def enough_samples(v, meow):
+    return len(v) >= meow
+
+
+def enough_time(v, day_delta):
+    return (v[-1] - v[0]) >= day_delta
+
+
+def determine_num_coefs(v, p):
+    span = v.shape[0] / p.NUM_OBS_FACTOR
+    if span < p.COEFFICIENT_MID:
+        return p.COEFFICIENT_MIN
+    elif span < p.COEFFICIENT_MAX:
+        return p.COEFFICIENT_MID
+    return p.COEFFICIENT_MAX
+
+
+def update_processing_mask(mask, index, window=None):
+    new_mask = mask.copy()
+    sub = new_mask[new_mask]
+    if window is not None:
+        w = sub[window]
+        w[index] = False
+        sub[window] = w
+    else:
+        sub[index] = False
+    new_mask[new_mask] = sub
+    return new_mask
+
+
+def find_closest_doy(dates, date_idx, window, num):
+    d_rt = dates[window] - dates[date_idx]
+    d_yr = np.abs(np.round(d_rt / 365.25) * 365.25 - d_rt)
+    return np.argsort(d_yr, kind='stable')[:num]
+
+
+def change_magnitude(residuals, variogram, comp_rmse):
+    rmse = np.maximum(variogram, comp_rmse)
+    mags = residuals / rmse[:, None]
+    return np.sum(mags * mags, axis=0)
+
+
+def detect_change(mags, thr):
+    return np.min(mags) > thr
+
+
+def detect_outlier(mag, thr):
+    return mag > thr
+
+
+def adjustpeek(dates, defpeek):
+    """change.adjustpeek (ncompare): peek grows with observation density."""
+    if dates.shape[0] < 2:
+        return defpeek
+    delta = np.median(np.diff(dates))
+    adj = int(np.round(defpeek * 16 / delta))
+    return adj if adj > defpeek else defpeek
+
+
+def adjustchgthresh(peek, defpeek, prob, default_thresh):
+    if peek > defpeek:
+        pt_cg = 1 - (1 - prob) ** (defpeek / peek)
+        return float(_chi2.ppf(pt_cg, 5))
+    return default_thresh
+
+
+def stable(models, dates, variogram, t_cg, detection_bands):
+    check = []
+    for idx in detection_bands:
+        rmse_norm = max(variogram[idx], models[idx].rmse)
+        slope = models[idx].coef[0] * (dates[-1] - dates[0])
+        check.append((abs(slope) + abs(models[idx].residual[0])
+                      + abs(models[idx].residual[-1])) / rmse_norm)
+    return euclidean_norm(check) < t_cg
+
+
+def results_to_changemodel(fitted_models, start_day, end_day, break_day, magnitudes,
+                           observation_count, change_probability, curve_qa):
+    out = {'start_day': int(start_day), 'end_day': int(end_day), 'break_day': int(break_day),
+           'observation_count': int(observation_count),
+           'change_probability': float(change_probability), 'curve_qa': int(curve_qa)}
+    for ix, m in enumerate(fitted_models):
+        out[BANDS[ix]] = {'magnitude': float(magnitudes[ix]), 'rmse': float(m.rmse),
+                          'coefficients': tuple(float(x) for x in m.coef),
+                          'intercept': float(m.intercept)}
+    return out
+
+
+def initialize(dates, observations, model_window, processing_mask, variogram, p):
+    period = dates[processing_mask]
+    spectral_obs = observations[:, processing_mask]
+    models = None
+    while model_window.stop + p.MEOW_SIZE < period.shape[0]:
+        if not enough_time(period[model_window], p.DAY_DELTA):
+            model_window = slice(model_window.start, model_window.stop + 1)
+            continue
+        tmask_outliers = tmask(period[model_window], spectral_obs[:, model_window], variogram, p)
+        tmask_count = int(np.sum(tmask_outliers))
+        tmask_period = period[model_window][~tmask_outliers]
+        if tmask_count == model_window.stop - model_window.start:
+            model_window = slice(model_window.start, model_window.stop + 1)
+            continue
+        if not enough_time(tmask_period, p.DAY_DELTA) or not enough_samples(tmask_period, p.MEOW_SIZE):
+            model_window = slice(model_window.start, model_window.stop + 1)
+            continue
+        if tmask_count:
+            processing_mask = update_processing_mask(processing_mask, tmask_outliers, model_window)
+            model_window = slice(model_window.start, model_window.stop - tmask_count)
+            period = dates[processing_mask]
+            spectral_obs = observations[:, processing_mask]
+        models = [fitted_model(period[model_window], s, p, 4) for s in spectral_obs[:, model_window]]
+        if not stable(models, period[model_window], variogram, p.CHANGE_THRESHOLD, p.DETECTION_BANDS):
+            model_window = slice(model_window.start + 1, model_window.stop + 1)
+            models = None
+            continue
+        break
+    return model_window, models, processing_mask
+
+
+def lookforward(dates, observations, model_window, processing_mask, variogram, p):
+    peek_size = p.PEEK_SIZE
+    fit_window = model_window
+    models = None
+    change = 0
+    period = dates[processing_mask]
+    spectral_obs = observations[:, processing_mask]
+    fit_span = period[model_window.stop - 1] - period[model_window.start]
+    residuals = None
+    num_coefs = p.COEFFICIENT_MIN
+    peek_window = slice(model_window.stop, model_window.stop + peek_size)
+    db = list(p.DETECTION_BANDS)
+    while model_window.stop + peek_size < period.shape[0] or models is None:
+        num_coefs = determine_num_coefs(period[model_window], p)
+        peek_window = slice(model_window.stop, model_window.stop + peek_size)
+        model_span = period[model_window.stop - 1] - period[model_window.start]
+        if not models or model_window.stop - model_window.start < 24:
+            fit_window = model_window
+            fit_span = period[model_window.stop - 1] - period[model_window.start]
+            models = [fitted_model(period[fit_window], s, p, num_coefs) for s in spectral_obs[:, fit_window]]
+            residuals = np.array([spectral_obs[i, peek_window] - predict(models[i], period[peek_window], p)
+                                  for i in range(observations.shape[0])])
+            comp_rmse = np.array([models[i].rmse for i in db])
+        else:
+            if model_span >= 1.33 * fit_span:
+                fit_window = model_window
+                fit_span = period[model_window.stop - 1] - period[model_window.start]
+                models = [fitted_model(period[fit_window], s, p, num_coefs) for s in spectral_obs[:, fit_window]]
+            residuals = np.array([spectral_obs[i, peek_window] - predict(models[i], period[peek_window], p)
+                                  for i in range(observations.shape[0])])
+            closest = find_closest_doy(period, peek_window.stop - 1, fit_window, 24)
+            comp_rmse = np.array([euclidean_norm(models[i].residual[closest]) / 4 for i in db])
+        magnitude = change_magnitude(residuals[db, :], variogram[db], comp_rmse)
+        if detect_change(magnitude, p.CHANGE_THRESHOLD):
+            change = 1
+            break
+        elif detect_outlier(magnitude[0], p.OUTLIER_THRESHOLD):
+            processing_mask = update_processing_mask(processing_mask, peek_window.start)
+            period = dates[processing_mask]
+            spectral_obs = observations[:, processing_mask]
+            continue
+        model_window = slice(model_window.start, model_window.stop + 1)
+    result = results_to_changemodel(
+        fitted_models=models, start_day=period[model_window.start],
+        end_day=period[model_window.stop - 1], break_day=period[peek_window.start],
+        magnitudes=np.median(residuals, axis=1),
+        observation_count=model_window.stop - model_window.start,
+        change_probability=change, curve_qa=num_coefs)
+    return result, processing_mask, model_window
+
+
+def lookback(dates, observations, model_window, models, previous_break, processing_mask, variogram, p):
+    peek_size = p.PEEK_SIZE
+    db = list(p.DETECTION_BANDS)
+    period = dates[processing_mask]
+    spectral_obs = observations[:, processing_mask]
+    while model_window.start > previous_break:
+        if model_window.start - previous_break > peek_size:
+            peek_window = slice(model_window.start - 1, model_window.start - peek_size, -1)
+        elif model_window.start - peek_size <= 0:
+            peek_window = slice(model_window.start - 1, None, -1)
+        else:
+            peek_window = slice(model_window.start - 1, previous_break - 1, -1)
+        residuals = np.array([spectral_obs[i][peek_window] - predict(models[i], period[peek_window], p)
+                              for i in range(observations.shape[0])])
+        comp_rmse = np.array([models[i].rmse for i in db])
+        magnitude = change_magnitude(residuals[db, :], variogram[db], comp_rmse)
+        if detect_change(magnitude, p.CHANGE_THRESHOLD):
+            break
+        elif detect_outlier(magnitude[0], p.OUTLIER_THRESHOLD):
+            processing_mask = update_processing_mask(processing_mask, peek_window.start)
+            period = dates[processing_mask]
+            spectral_obs = observations[:, processing_mask]
+            model_window = slice(model_window.start - 1, model_window.stop - 1)
+            continue
+        model_window = slice(peek_window.start, model_window.stop)
+    return model_window, processing_mask
+
+
+def catch(dates, observations, processing_mask, model_window, curve_qa, p):
+    period = dates[processing_mask]
+    spectral_obs = observations[:, processing_mask]
+    models = [fitted_model(period[model_window], s, p, p.COEFFICIENT_MIN)
+              for s in spectral_obs[:, model_window]]
+    try:
+        break_day = period[model_window.stop]
+    except IndexError:
+        break_day = period[-1]
+    return results_to_changemodel(
+        fitted_models=models, start_day=period[model_window.start],
+        end_day=period[model_window.stop - 1], break_day=break_day,
+        magnitudes=np.zeros(7), observation_count=model_window.stop - model_window.start,
+        change_probability=0, curve_qa=curve_qa)
+
+
+# --------------------------------------------------------------------------- procedures.py [ext]
+def standard_procedure(dates, observations, quality, p):
+    meow_size = p.MEOW_SIZE
+    defpeek = p.PEEK_SIZE
+    if p.KELVIN_TO_CELSIUS:
+        observations[p.THERMAL_IDX] = kelvin_to_celsius(observations[p.THERMAL_IDX])
+    processing_mask = standard_procedure_filter(observations, quality, dates, p)
+    results = []
+    model_window = slice(0, meow_size)
+    previous_end = 0
+    start = True
+    variogram = adjusted_variogram(dates[processing_mask], observations[:, processing_mask])
+    peek_size = defpeek
+    if p.ADAPTIVE_PEEK:
+        peek_size = adjustpeek(dates[processing_mask], defpeek)
+        p.CHANGE_THRESHOLD = adjustchgthresh(peek_size, defpeek, p.CHANGE_PROBABILITY,
+                                             p.CHANGE_THRESHOLD)
+        p.PEEK_SIZE = peek_size
+    while model_window.stop <= dates[processing_mask].shape[0] - meow_size:
+        if len(results) > 0:
+            start = False
+        model_window, init_models, processing_mask = initialize(
+            dates, observations, model_window, processing_mask, variogram, p)
+        if init_models is None:
+            break
+        if model_window.start > previous_end:
+            model_window, processing_mask = lookback(
+                dates, observations, model_window, init_models, previous_end,
+                processing_mask, variogram, p)
+        if model_window.start - previous_end > peek_size and start is True:
+            results.append(catch(dates, observations, processing_mask,
+                                 slice(previous_end, model_window.start), p.CURVE_QA['START'], p))
+            start = False
+        if model_window.stop + peek_size > dates[processing_mask].shape[0]:
+            break
+        result, processing_mask, model_window = lookforward(
+            dates, observations, model_window, processing_mask, variogram, p)
+        results.append(result)
+        previous_end = model_window.stop
+        model_window = slice(model_window.stop, model_window.stop + meow_size)
+    if previous_end + peek_size < dates[processing_mask].shape[0]:
+        model_window = slice(previous_end, dates[processing_mask].shape[0])
+        results.append(catch(dates, observations, processing_mask, model_window,
+                             p.CURVE_QA['END'], p))
+    return results, processing_mask
+
+
+def _single_model_procedure(dates, observations, quality, p, filt, curve_qa):
+    processing_mask = filt(observations, quality, dates, p)
+    period = dates[processing_mask]
+    spectral_obs = observations[:, processing_mask]
+    if np.sum(processing_mask) < p.MEOW_SIZE:
+        return [], processing_mask
+    models = [fitted_model(period, s, p, p.COEFFICIENT_MIN) for s in spectral_obs]
+    result = results_to_changemodel(
+        fitted_models=models, start_day=dates[0], end_day=dates[-1], break_day=0,
+        magnitudes=np.zeros(7), observation_count=int(np.sum(processing_mask)),
+        change_probability=0, curve_qa=curve_qa)
+    return [result], processing_mask
+
+
+def permanent_snow_procedure(dates, observations, quality, p):
+    return _single_model_procedure(dates, observations, quality, p, snow_procedure_filter,
+                                   p.CURVE_QA['PERSIST_SNOW'])
+
+
+def insufficient_clear_procedure(dates, observations, quality, p):
+    return _single_model_procedure(dates, observations, quality, p, insufficient_clear_filter,
+                                   p.CURVE_QA['INSUF_CLEAR'])
+
+
+PROCEDURES = {'standard_procedure': 0, 'permanent_snow_procedure': 1,
+              'insufficient_clear_procedure': 2}
+
+
+def fit_procedure(quality, p):
+    if not enough_clear(quality, p):
+        if enough_snow(quality, p):
+            return permanent_snow_procedure
+        return insufficient_clear_procedure
+    return standard_procedure
+
+
+# --------------------------------------------------------------------------- ccd/__init__.py [ext]
+def detect(dates, blues, greens, reds, nirs, swir1s, swir2s, thermals, qas, params=None):
+    """ccd.detect restated (called at reference ccdc/pyccd.py:168)."""
+    p = get_params(params)
+    dates = np.asarray(dates)
+    qas = np.asarray(qas)
+    spectra = np.stack((blues, greens, reds, nirs, swir1s, swir2s, thermals))
+    assert dates.ndim == 1 and dates.shape == qas.shape and dates.shape[0] == spectra.shape[1]
+    indices = np.argsort(dates, kind='stable')
+    dates = dates[indices]
+    spectra = spectra[:, indices]
+    qas = qas[indices]
+    if p.QA_BITPACKED:
+        qas = unpackqa(qas, p)
+    probs = quality_probabilities(qas, p)
+    procedure = fit_procedure(qas, p)
+    change_models, processing_mask = procedure(dates, spectra, qas, p)
+    return {'algorithm': ALGORITHM,
+            'processing_mask': [int(x) for x in processing_mask],
+            'procedure': procedure.__name__,
+            'change_models': list(change_models),
+            'cloud_prob': probs[0], 'snow_prob': probs[1], 'water_prob': probs[2]}
