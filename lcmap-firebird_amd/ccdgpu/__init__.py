@@ -1,0 +1,198 @@
+"""ctypes binding of libccdgpu.so (include/ccdgpu.h) -- the MI355X change-detection backend.
+
+This is the only way the Python host side reaches the GPU: plain pointers and sizes through the
+C-ABI, no torch types.  The library must be built (``__graft_entry__.build()`` / ``make -C
+lcmap-firebird_amd``); if it is missing or no gfx950 device is visible, every call raises
+``CcdGpuError`` -- there is no CPU fallback on the product path.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+from . import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), 'lib', 'libccdgpu.so')
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+class CcdGpuError(RuntimeError):
+    def __init__(self, code, message):
+        super().__init__('ccdgpu error %d: %s' % (code, message))
+        self.code = code
+        self.message = message
+
+
+class QAValueError(ValueError):
+    """Unsupported bit-packed QA value: the analogue of pyccd qa.qabitval's ValueError."""
+
+
+def _declare(L):
+    c = ctypes
+    L.ccdgpu_version.restype = c.c_char_p
+    L.ccdgpu_last_error.restype = c.c_char_p
+    L.ccdgpu_params_default.argtypes = [c.POINTER(abi.Params)]
+    L.ccdgpu_init.argtypes = [c.c_int, c.POINTER(c.c_void_p)]
+    L.ccdgpu_destroy.argtypes = [c.c_void_p]
+    L.ccdgpu_device_count.argtypes = [c.POINTER(c.c_int)]
+    L.ccdgpu_synchronize.argtypes = [c.c_void_p]
+    L.ccdgpu_detect_batch.argtypes = [c.c_void_p, c.POINTER(abi.Params), c.c_int32, c.c_int32,
+                                      c.c_void_p, c.c_void_p, c.c_void_p, c.POINTER(abi.Result)]
+    L.ccdgpu_result_free.argtypes = [c.POINTER(abi.Result)]
+    L.ccdgpu_stage.argtypes = [c.c_void_p, c.POINTER(abi.Params), c.c_int32, c.c_int32, c.c_int32,
+                               c.c_void_p, c.c_void_p, c.c_void_p]
+    L.ccdgpu_run_staged.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
+    L.ccdgpu_fetch_staged.argtypes = [c.c_void_p, c.c_int32, c.POINTER(abi.Result)]
+    L.ccdgpu_last_stats.argtypes = [c.c_void_p, c.POINTER(abi.Stats)]
+    for name in ('ccdgpu_init', 'ccdgpu_destroy', 'ccdgpu_device_count', 'ccdgpu_synchronize',
+                 'ccdgpu_detect_batch', 'ccdgpu_stage', 'ccdgpu_run_staged', 'ccdgpu_fetch_staged',
+                 'ccdgpu_last_stats'):
+        getattr(L, name).restype = c.c_int
+    return L
+
+
+EXPORTS = ('ccdgpu_version', 'ccdgpu_last_error', 'ccdgpu_params_default', 'ccdgpu_init',
+           'ccdgpu_destroy', 'ccdgpu_device_count', 'ccdgpu_synchronize', 'ccdgpu_detect_batch',
+           'ccdgpu_result_free', 'ccdgpu_stage', 'ccdgpu_run_staged', 'ccdgpu_fetch_staged',
+           'ccdgpu_last_stats')
+
+
+def lib():
+    """Load libccdgpu.so (raises CcdGpuError if it has not been built)."""
+    global _lib
+    with _lib_lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise CcdGpuError(abi.E_HIP, 'libccdgpu.so not built at %s (run __graft_entry__.build())' % LIB_PATH)
+            _lib = _declare(ctypes.CDLL(LIB_PATH))
+    return _lib
+
+
+def last_error():
+    return lib().ccdgpu_last_error().decode()
+
+
+def _check(rc):
+    if rc == abi.E_QA:
+        raise QAValueError(last_error())
+    if rc != 0:
+        raise CcdGpuError(rc, last_error())
+
+
+def version():
+    return lib().ccdgpu_version().decode()
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    rc = lib().ccdgpu_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0
+
+
+def default_params():
+    p = abi.Params()
+    lib().ccdgpu_params_default(ctypes.byref(p))
+    return p
+
+
+def _as_inputs(dates, spectra, qa):
+    dates = np.ascontiguousarray(dates, dtype=np.int64)
+    spectra = np.ascontiguousarray(spectra, dtype=np.int16)
+    qa = np.ascontiguousarray(qa, dtype=np.uint16)
+    return dates, spectra, qa
+
+
+class Context(object):
+    """One HIP device + stream (ccdgpu_ctx).  Not shared across threads."""
+
+    def __init__(self, device=0):
+        self._ctx = ctypes.c_void_p()
+        _check(lib().ccdgpu_init(int(device), ctypes.byref(self._ctx)))
+        self.device = device
+
+    def close(self):
+        if self._ctx:
+            lib().ccdgpu_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def synchronize(self):
+        _check(lib().ccdgpu_synchronize(self._ctx))
+
+    def detect_batch(self, dates, spectra, qa, params=None):
+        """Pixels sharing one date vector: dates [n], spectra [7][n_pix][n], qa [n_pix][n].
+        Returns abi.Unpacked.  Raises QAValueError on unsupported QA values."""
+        dates, spectra, qa = _as_inputs(dates, spectra, qa)
+        n_pix, n_obs = qa.shape
+        if spectra.shape != (7, n_pix, n_obs) or dates.shape != (n_obs,):
+            raise ValueError('shape mismatch: dates %s spectra %s qa %s' % (dates.shape, spectra.shape, qa.shape))
+        p = params if isinstance(params, abi.Params) else abi.params_from_dict(params)
+        res = abi.Result()
+        rc = lib().ccdgpu_detect_batch(self._ctx, ctypes.byref(p), n_pix, n_obs, dates.ctypes.data,
+                                       spectra.ctypes.data, qa.ctypes.data, ctypes.byref(res))
+        try:
+            if rc not in (0, abi.E_QA):
+                _check(rc)
+            u = abi.unpack(res)
+        finally:
+            lib().ccdgpu_result_free(ctypes.byref(res))
+        if rc == abi.E_QA:
+            err = QAValueError(last_error())
+            err.result = u
+            raise err
+        return u
+
+    # device-resident path ------------------------------------------------------------------
+    def stage(self, dates, spectra, qa, params=None):
+        """dates [C][n], spectra [C][7][n_pix][n], qa [C][n_pix][n] -> staged on the device."""
+        dates, spectra, qa = _as_inputs(dates, spectra, qa)
+        n_chips, n_pix, n_obs = qa.shape
+        p = params if isinstance(params, abi.Params) else abi.params_from_dict(params)
+        _check(lib().ccdgpu_stage(self._ctx, ctypes.byref(p), n_chips, n_pix, n_obs,
+                                  dates.ctypes.data, spectra.ctypes.data, qa.ctypes.data))
+        self._keep = (dates, spectra, qa)
+
+    def run(self):
+        secs = ctypes.c_double(0.0)
+        rc = lib().ccdgpu_run_staged(self._ctx, ctypes.byref(secs))
+        if rc not in (0, abi.E_QA):
+            _check(rc)
+        return secs.value
+
+    def fetch(self, chip):
+        res = abi.Result()
+        rc = lib().ccdgpu_fetch_staged(self._ctx, int(chip), ctypes.byref(res))
+        try:
+            _check(rc)
+            return abi.unpack(res)
+        finally:
+            lib().ccdgpu_result_free(ctypes.byref(res))
+
+    def stats(self):
+        s = abi.Stats()
+        _check(lib().ccdgpu_last_stats(self._ctx, ctypes.byref(s)))
+        return {k: getattr(s, k) for k, _ in abi.Stats._fields_}
+
+
+_default_ctx = {}
+
+
+def default_context(device=None):
+    """Per-thread default context on ``device`` (HIP_VISIBLE_DEVICES-relative, default 0)."""
+    if device is None:
+        device = int(os.environ.get('CCDGPU_DEVICE', '0'))
+    key = (threading.get_ident(), device)
+    ctx = _default_ctx.get(key)
+    if ctx is None:
+        ctx = Context(device)
+        _default_ctx[key] = ctx
+    return ctx

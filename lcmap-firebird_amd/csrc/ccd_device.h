@@ -1,0 +1,67 @@
+// ccd_device.h -- device-side data contract shared by the HIP kernels and the host API.
+//
+// Layout in HBM (one "staged batch" = n_chips chips of n_pix pixels x n_obs observations):
+//   dates     int64 [n_chips][n_obs]            input order (merlin: descending)
+//   spectra   int16 [n_chips][7][n_pix][n_obs]  band-major, observation-contiguous (ABI layout)
+//   qa        uint16[n_chips][n_pix][n_obs]
+//   order     int32 [n_chips][n_obs]            sorted position -> input position (stable)
+//   sdates    int64 [n_chips][n_obs]            sorted dates
+//   basis     f64   [n_chips][n_obs][8]         t, cos wt, sin wt, cos 2wt, sin 2wt, cos 3wt, sin 3wt, 0
+//                                               (models/lasso.coefficient_matrix rows, shared by
+//                                                all 10^4 pixels of a chip)
+//   per wave slot scratch (persistent grid): compacted period of the current pixel
+//     cdate int32[n_obs], cidx uint16[n_obs], cval int16[7][n_obs]  (20 B / observation)
+//   outputs: mask bits, procedure, probs, per-pixel segment count, segment pool (+ seq numbers)
+#pragma once
+#include <stdint.h>
+
+#include "../../include/ccdgpu.h"
+
+#define CCD_NB 7
+#define CCD_WAVE 64
+#define CCD_BASIS_STRIDE 8
+
+struct CcdDetectArgs {
+    ccdgpu_params p;
+    int32_t n_chips, n_pix, n_obs, mask_words;
+    int32_t n_slots;
+    int32_t pad0;
+    int64_t total_pix;
+    int64_t pool_cap;
+    const int16_t *spectra;
+    const uint16_t *qa;
+    const int32_t *order;
+    const int64_t *sdates;
+    const double *basis;
+    // work queue + global flags: [0] next pixel, [1] pool count, [2] error pixel+1 (min), [3] overflow
+    unsigned long long *counters;
+    // per-slot scratch
+    int32_t *s_date;
+    uint16_t *s_idx;
+    int16_t *s_val;
+    double *s_f64;   // [n_slots][5][n_obs] Tmask scratch
+    // outputs
+    uint32_t *mask_bits;
+    int32_t *procedure;
+    double *probs;
+    int32_t *nseg;
+    ccdgpu_segment *pool;
+    int32_t *pool_seq;
+    // instrumentation: [0] fits (band models), [1] CD sweeps, [2] counted flops
+    unsigned long long *stats;
+    // change threshold per (adaptive) peek size, index = peek (<= CCDGPU_MAX_PEEK)
+    double thr_table[CCDGPU_MAX_PEEK + 1];
+};
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+// kernel launchers (ccd_kernels.hip)
+int ccdk_prep(const int64_t *dates, int32_t n_chips, int32_t n_obs, double avg_days_yr,
+              int32_t *order, int64_t *sdates, double *basis, void *stream);
+int ccdk_detect(const CcdDetectArgs *dev_args, int32_t grid, void *stream);
+int ccdk_scatter(const ccdgpu_segment *pool, const int32_t *pool_seq, int64_t n_pool,
+                 const int64_t *offsets, int32_t n_pix_per_chip, ccdgpu_segment *out, void *stream);
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,1251 @@
+// ccd_kernels.hip -- MI355X (gfx950) CCDC change detection: the whole per-pixel pyccd state
+// machine on device, one wavefront per pixel.
+//
+// What runs here (reference: ccd.detect called at ccdc/pyccd.py:168; pyccd module names in the
+// comments are lcmap-pyccd 2018.03.12.dev-ncompare.b2, restated in oracle/ccd_ref.py):
+//   ccdk_prep    -- per chip: stable argsort of the acquisition dates (ccd/__init__.py detect) and
+//                   the Lasso design rows cos/sin(k w t) (models/lasso.coefficient_matrix), shared
+//                   by every pixel of the chip.
+//   ccd_detect   -- persistent kernel, one 64-lane wavefront per pixel pulled from a device work
+//                   queue (active-pixel compaction: a wave that finishes a short pixel takes the
+//                   next one, so divergent pixels never idle lanes of a long one):
+//                   QA unpack/filter/dedup + compaction (qa.py), variogram (math_utils.py),
+//                   ncompare peek (change.py), initialize + Tmask IRLS (procedures.py,
+//                   models/tmask.py, models/robust_fit.py), stability (change.stable), lookback,
+//                   lookforward with closest-DOY comparison RMSE, catch (change.py), 4/6/8-coef
+//                   Lasso (models/lasso.py = sklearn 0.18 coordinate descent, here in Gram form),
+//                   permanent-snow / insufficient-clear single fits (procedures.py).
+//   ccdk_scatter -- segment pool -> CSR by pixel.
+//
+// Parallel mapping inside a wave (all control flow is wave-uniform; every reduction is a
+// shuffle butterfly whose result is bit-identical in all lanes):
+//   * observation loops: lane = observation (coalesced loads of the compacted period);
+//   * Gram build: design rows staged in LDS, lane = Gram / X'y entry, sequential over rows;
+//   * coordinate descent: lane = band (7 independent Lasso problems sharing one Gram);
+//   * medians / 24-closest selection: counting selection with ballots (no sorting);
+//   * peek windows: lane = peek observation.
+// FP64 vector ALU throughout (tiny latency-bound solves; no MFMA shape exists).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "ccd_device.h"
+
+namespace {
+
+constexpr int NB = CCD_NB;
+constexpr int W = CCD_WAVE;
+constexpr int RW = 16;  // doubles per staged design row: t c1 s1 c2 s2 c3 s3 _ y0..y6 _
+constexpr int MAXW = CCDGPU_MAX_OBS / 32;
+
+struct Lds {
+    double row[W][RW];
+    double G[8][8];
+    double Q[8][8];  // Q[j][band] = Xc_j . yc_band
+    double YY[8];
+    double xm[8];
+    double ym[8];
+    double coef[NB][8];  // [band][0..6] = w, [band][7] = intercept
+    double rmse[8];
+    double vario[8];
+    uint32_t mask[MAXW];   // processing mask, sorted order
+    uint32_t tflag[MAXW];  // Tmask outlier flags of the current window
+};
+
+struct Px {
+    const CcdDetectArgs *A;
+    Lds *L;
+    int n;      // observations (sorted)
+    int m;      // current compacted period length
+    int peek;   // (adaptive) peek size
+    double chg; // change threshold
+    const double *basis;
+    const int64_t *sd;
+    int32_t *cd;
+    uint16_t *ci;
+    int16_t *cv;
+    double *fs;  // per-slot double scratch [5][n]
+    int64_t gpix;
+    int nseg;
+    unsigned long long fits, sweeps;
+};
+
+// ------------------------------------------------------------------ wave primitives
+__device__ __forceinline__ int lane() { return (int)__lane_id(); }
+__device__ __forceinline__ unsigned long long bal(bool p) { return __ballot(p); }
+__device__ __forceinline__ int popc(unsigned long long x) { return __popcll(x); }
+__device__ __forceinline__ int below(unsigned long long m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
+}
+__device__ __forceinline__ double wsum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ void wsync() { __syncthreads(); }
+
+__device__ __forceinline__ double cvalf(const Px &P, int b, int j) { return (double)P.cv[(size_t)b * P.n + j]; }
+
+// k-th smallest (0-based) of integer values in [lo, hi] produced by gen(i, &v) (returns valid).
+template <class F>
+__device__ int kth_int(F gen, int N, int k, int lo, int hi) {
+    const int l = lane();
+    while (lo < hi) {
+        const int mid = lo + ((hi - lo) >> 1);
+        int c = 0;
+        for (int base = 0; base < N; base += W) {
+            const int i = base + l;
+            int v = 0;
+            bool ok = false;
+            if (i < N) ok = gen(i, v);
+            c += popc(bal(ok && v <= mid));
+        }
+        if (c >= k + 1) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo;
+}
+
+template <class F>
+__device__ double median_int(F gen, int N, int cnt, int lo, int hi) {
+    if (cnt <= 0) return __builtin_nan("");
+    if (cnt & 1) return (double)kth_int(gen, N, cnt / 2, lo, hi);
+    const int a = kth_int(gen, N, cnt / 2 - 1, lo, hi);
+    const int b = kth_int(gen, N, cnt / 2, lo, hi);
+    return ((double)a + (double)b) / 2.0;
+}
+
+// k-th smallest of non-negative doubles vals[0..N) (bit patterns are monotone for x >= 0).
+__device__ double kth_nonneg(const double *vals, int N, int k) {
+    const int l = lane();
+    unsigned long long lo = 0ull, hi = 0x7FF0000000000000ull;
+    while (lo < hi) {
+        const unsigned long long mid = lo + ((hi - lo) >> 1);
+        int c = 0;
+        for (int base = 0; base < N; base += W) {
+            const int i = base + l;
+            bool ok = false;
+            if (i < N) ok = (unsigned long long)__double_as_longlong(vals[i]) <= mid;
+            c += popc(bal(ok));
+        }
+        if (c >= k + 1) hi = mid;
+        else lo = mid + 1;
+    }
+    return __longlong_as_double((long long)lo);
+}
+
+__device__ __forceinline__ int qabitval(const ccdgpu_params &p, unsigned v) {
+#define BIT(o) ((v >> (o)) & 1u)
+    if (BIT(p.qa_fill)) return p.qa_fill;
+    if (BIT(p.qa_cloud)) return p.qa_cloud;
+    if (BIT(p.qa_shadow)) return p.qa_shadow;
+    if (BIT(p.qa_snow)) return p.qa_snow;
+    if (BIT(p.qa_water)) return p.qa_water;
+    if (BIT(p.qa_clear)) return p.qa_clear;
+    if (BIT(p.qa_cirrus1) && BIT(p.qa_cirrus2)) return p.qa_clear;
+    if (BIT(p.qa_occlusion)) return p.qa_clear;
+    return -1;
+#undef BIT
+}
+
+// ------------------------------------------------------------------ compaction
+// Drop observations of [a, m) for which drop(j) is true (j = compacted index, valid only for the
+// caller's range); the tail is shifted down in one ascending pass (writes never overtake reads).
+template <class F>
+__device__ int compact_drop(Px &P, int a, F drop) {
+    const int l = lane();
+    int out = a;
+    for (int base = a; base < P.m; base += W) {
+        const int j = base + l;
+        const bool in = j < P.m;
+        int32_t d = 0;
+        uint16_t c = 0;
+        int16_t v[NB];
+        bool dr = false;
+        if (in) {
+            d = P.cd[j];
+            c = P.ci[j];
+#pragma unroll
+            for (int b = 0; b < NB; ++b) v[b] = P.cv[(size_t)b * P.n + j];
+            dr = drop(j);
+        }
+        const unsigned long long keep = bal(in && !dr);
+        if (in && dr) atomicAnd(&P.L->mask[c >> 5], ~(1u << (c & 31)));
+        if (in && !dr) {
+            const int pos = out + below(keep);
+            P.cd[pos] = d;
+            P.ci[pos] = c;
+#pragma unroll
+            for (int b = 0; b < NB; ++b) P.cv[(size_t)b * P.n + pos] = v[b];
+        }
+        out += popc(keep);
+    }
+    P.m = out;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    wsync();
+    return out;
+}
+
+// ------------------------------------------------------------------ Lasso (models/lasso.py)
+__device__ __forceinline__ void stage_rows(const Px &P, int j0, int cnt) {
+    const int l = lane();
+    if (l < cnt) {
+        const int j = j0 + l;
+        const double *bs = P.basis + (size_t)P.ci[j] * CCD_BASIS_STRIDE;
+        double *r = P.L->row[l];
+        r[0] = (double)P.cd[j];
+#pragma unroll
+        for (int c = 1; c < 7; ++c) r[c] = bs[c];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) r[8 + b] = cvalf(P, b, j);
+    }
+    wsync();
+}
+
+// sklearn 0.18 enet_coordinate_descent (beta = 0, cyclic) in Gram form for PC active columns.
+template <int PC>
+__device__ int cd_gram(const Lds *L, int band, double alpha, int max_iter, double tol, double *wout) {
+    double g[PC][PC], q[PC], w[PC];
+#pragma unroll
+    for (int j = 0; j < PC; ++j) {
+        q[j] = L->Q[j][band];
+        w[j] = 0.0;
+#pragma unroll
+        for (int k = 0; k < PC; ++k) g[j][k] = L->G[j][k];
+    }
+    const double yy = L->YY[band];
+    const double d_w_tol = tol;
+    const double tol_s = tol * yy;
+    int it = 0;
+    for (it = 0; it < max_iter; ++it) {
+        double w_max = 0.0, d_w_max = 0.0;
+#pragma unroll
+        for (int j = 0; j < PC; ++j) {
+            if (g[j][j] == 0.0) continue;
+            double tmp = q[j];
+#pragma unroll
+            for (int k = 0; k < PC; ++k)
+                if (k != j) tmp -= g[j][k] * w[k];
+            const double aa = fabs(tmp) - alpha;
+            const double wn = aa > 0.0 ? (tmp > 0.0 ? aa : -aa) / g[j][j] : 0.0;
+            const double d = fabs(wn - w[j]);
+            w[j] = wn;
+            d_w_max = d > d_w_max ? d : d_w_max;
+            w_max = fabs(wn) > w_max ? fabs(wn) : w_max;
+        }
+        if (w_max == 0.0 || d_w_max / w_max < d_w_tol || it == max_iter - 1) {
+            double dual = 0.0, wq = 0.0, wxta = 0.0, l1 = 0.0;
+#pragma unroll
+            for (int j = 0; j < PC; ++j) {
+                double gw = 0.0;
+#pragma unroll
+                for (int k = 0; k < PC; ++k) gw += g[j][k] * w[k];
+                const double xta = q[j] - gw;
+                dual = fabs(xta) > dual ? fabs(xta) : dual;
+                wq += w[j] * q[j];
+                wxta += w[j] * xta;
+                l1 += fabs(w[j]);
+            }
+            const double ry = yy - wq;        // R . y
+            const double rr = ry - wxta;      // R . R = yy - 2 w.q + w.G.w
+            double cst, gap;
+            if (dual > alpha) {
+                cst = alpha / dual;
+                gap = 0.5 * (rr + rr * cst * cst);
+            } else {
+                cst = 1.0;
+                gap = rr;
+            }
+            gap += alpha * l1 - cst * ry;
+            if (gap < tol_s) break;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < PC; ++j) wout[j] = w[j];
+    return (it < max_iter ? it : max_iter - 1) + 1;
+}
+
+// lasso.fitted_model for the 7 bands over compacted window [a, b) with k coefficients.
+__device__ void fit_models(Px &P, int a, int b, int k) {
+    const ccdgpu_params &p = P.A->p;
+    Lds *L = P.L;
+    const int l = lane();
+    const int nw = b - a;
+    const int pc = k - 1;  // active design columns (t + harmonics)
+    // pass 1: column means (x columns 0..6, y bands) -- sequential per column, lane = column
+    double acc = 0.0;
+    for (int t0 = 0; t0 < nw; t0 += W) {
+        const int cnt = nw - t0 < W ? nw - t0 : W;
+        stage_rows(P, a + t0, cnt);
+        if (l < 14) {
+            const int col = l < 7 ? l : l + 1;
+            for (int r = 0; r < cnt; ++r) acc += L->row[r][col];
+        }
+        wsync();
+    }
+    if (l < 7) L->xm[l] = acc / nw;
+    else if (l < 14) L->ym[l - 7] = acc / nw;
+    wsync();
+    // pass 2: centred Gram entries; lane handles entries e = l and l + 64
+    const int nG = pc * (pc + 1) / 2;
+    const int nE = nG + 7 * pc + 7;
+    int ca[2], cb[2];
+    double ma[2], mb[2], s[2] = {0.0, 0.0};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        int e = l + h * W;
+        ca[h] = cb[h] = -1;
+        ma[h] = mb[h] = 0.0;
+        if (e < nG) {
+            int j = 0;
+            while (e >= pc - j) { e -= pc - j; ++j; }
+            ca[h] = j;
+            cb[h] = j + e;
+        } else if (e < nG + 7 * pc) {
+            e -= nG;
+            ca[h] = e / 7;        // design column
+            cb[h] = 8 + e % 7;    // y band
+        } else if (e < nE) {
+            e -= nG + 7 * pc;
+            ca[h] = cb[h] = 8 + e;
+        }
+        if (ca[h] >= 0) {
+            ma[h] = ca[h] < 8 ? L->xm[ca[h]] : L->ym[ca[h] - 8];
+            mb[h] = cb[h] < 8 ? L->xm[cb[h]] : L->ym[cb[h] - 8];
+        }
+    }
+    for (int t0 = 0; t0 < nw; t0 += W) {
+        const int cnt = nw - t0 < W ? nw - t0 : W;
+        if (nw > W) stage_rows(P, a + t0, cnt);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (ca[h] >= 0) {
+                for (int r = 0; r < cnt; ++r)
+                    s[h] += (L->row[r][ca[h]] - ma[h]) * (L->row[r][cb[h]] - mb[h]);
+            }
+        }
+        wsync();
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (ca[h] >= 0) {
+            if (cb[h] < 8) {
+                L->G[ca[h]][cb[h]] = s[h];
+                L->G[cb[h]][ca[h]] = s[h];
+            } else if (ca[h] < 8) {
+                L->Q[ca[h]][cb[h] - 8] = s[h];
+            } else {
+                L->YY[ca[h] - 8] = s[h];
+            }
+        }
+    }
+    wsync();
+    // coordinate descent, lane = band
+    if (l < NB) {
+        double w[7] = {0, 0, 0, 0, 0, 0, 0};
+        const double alpha = p.lasso_alpha * nw;
+        int sw;
+        if (pc == 3) sw = cd_gram<3>(L, l, alpha, p.lasso_max_iter, p.lasso_tol, w);
+        else if (pc == 5) sw = cd_gram<5>(L, l, alpha, p.lasso_max_iter, p.lasso_tol, w);
+        else sw = cd_gram<7>(L, l, alpha, p.lasso_max_iter, p.lasso_tol, w);
+        double dot = 0.0;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) {
+            dot += L->xm[j] * w[j];
+            L->coef[l][j] = w[j];
+        }
+        L->coef[l][7] = L->ym[l] - dot;
+        P.sweeps += (unsigned long long)sw;  // per-lane; reduced at the end
+    }
+    P.fits += NB;
+    wsync();
+    // rmse from residuals of the raw design (predict = X @ coef + intercept)
+    double ss[NB] = {0, 0, 0, 0, 0, 0, 0};
+    for (int t0 = 0; t0 < nw; t0 += W) {
+        const int j = a + t0 + l;
+        if (t0 + l < nw) {
+            const double *bs = P.basis + (size_t)P.ci[j] * CCD_BASIS_STRIDE;
+            const double x0 = (double)P.cd[j];
+#pragma unroll
+            for (int band = 0; band < NB; ++band) {
+                const double *c = L->coef[band];
+                double pr = x0 * c[0];
+#pragma unroll
+                for (int jj = 1; jj < 7; ++jj) pr += bs[jj] * c[jj];
+                pr += c[7];
+                const double r = cvalf(P, band, j) - pr;
+                ss[band] += r * r;
+            }
+        }
+    }
+    const double den = (double)(nw - (p.rmse_dof ? k : 0));
+#pragma unroll
+    for (int band = 0; band < NB; ++band) {
+        const double t = wsum(ss[band]);
+        if (l == 0) L->rmse[band] = sqrt(t / den);
+    }
+    wsync();
+}
+
+// residual of band b at compacted observation j for the current models (lasso.predict)
+__device__ __forceinline__ double resid_at(const Px &P, int band, int j) {
+    const double *bs = P.basis + (size_t)P.ci[j] * CCD_BASIS_STRIDE;
+    const double *c = P.L->coef[band];
+    double pr = (double)P.cd[j] * c[0];
+#pragma unroll
+    for (int jj = 1; jj < 7; ++jj) pr += bs[jj] * c[jj];
+    pr += c[7];
+    return cvalf(P, band, j) - pr;
+}
+
+// ------------------------------------------------------------------ segment output
+__device__ void emit(Px &P, int sday, int eday, int bday, int count, double chprob, int cqa,
+                     double mag_lane /* lane b: magnitude of band b */) {
+    const CcdDetectArgs &A = *P.A;
+    const int l = lane();
+    unsigned long long slot = 0;
+    if (l == 0) slot = atomicAdd(&A.counters[1], 1ull);
+    slot = __shfl((unsigned long long)slot, 0);
+    if (slot >= (unsigned long long)A.pool_cap) {
+        if (l == 0) atomicOr(&A.counters[3], 1ull);
+        P.nseg++;
+        return;
+    }
+    ccdgpu_segment *s = A.pool + slot;
+    if (l < NB) {
+        s->magnitude[l] = mag_lane;
+        s->rmse[l] = P.L->rmse[l];
+        s->intercept[l] = P.L->coef[l][7];
+#pragma unroll
+        for (int j = 0; j < 7; ++j) s->coef[l][j] = P.L->coef[l][j];
+    }
+    if (l == 0) {
+        s->start_day = sday;
+        s->end_day = eday;
+        s->break_day = bday;
+        s->observation_count = count;
+        s->curve_qa = cqa;
+        s->pixel = (int32_t)P.gpix;
+        s->change_probability = chprob;
+        A.pool_seq[slot] = P.nseg;
+    }
+    P.nseg++;
+}
+
+__device__ void catch_(Px &P, int a, int b, int cqa) {
+    fit_models(P, a, b, P.A->p.coef_min);
+    const int bday = b < P.m ? P.cd[b] : P.cd[P.m - 1];
+    emit(P, P.cd[a], P.cd[b - 1], bday, b - a, 0.0, cqa, 0.0);
+}
+
+// ------------------------------------------------------------------ variogram / peek
+__device__ void variogram(Px &P) {
+    Lds *L = P.L;
+    const int l = lane();
+    const int m = P.m;
+    if (m < 2) {
+        if (l < NB) L->vario[l] = __builtin_nan("");
+        wsync();
+        return;
+    }
+    int lag = 0;
+    for (int k = 1; k < m; ++k) {
+        int cnt = 0;
+        for (int base = 0; base < m - k; base += W) {
+            const int i = base + l;
+            cnt += popc(bal(i < m - k && (P.cd[i + k] - P.cd[i]) > 30));
+        }
+        if (2 * cnt >= m - k) { lag = k; break; }
+    }
+    const int kk = lag ? lag : 1;
+    const bool all = lag == 0;
+    int cnt = 0;
+    for (int base = 0; base < m - kk; base += W) {
+        const int i = base + l;
+        cnt += popc(bal(i < m - kk && (all || (P.cd[i + kk] - P.cd[i]) > 30)));
+    }
+    for (int band = 0; band < NB; ++band) {
+        const int16_t *v = P.cv + (size_t)band * P.n;
+        auto gen = [&](int i, int &val) -> bool {
+            if (i >= m - kk) return false;
+            if (!all && (P.cd[i + kk] - P.cd[i]) <= 30) return false;
+            int d = (int)v[i + kk] - (int)v[i];
+            val = d < 0 ? -d : d;
+            return true;
+        };
+        const double med = median_int(gen, m - kk, cnt, 0, 65535);
+        if (l == 0) L->vario[band] = med;
+    }
+    wsync();
+}
+
+__device__ void adjust_peek(Px &P) {
+    const ccdgpu_params &p = P.A->p;
+    P.peek = p.peek_size;
+    P.chg = p.change_threshold;
+    if (!p.adaptive_peek || P.m < 2) return;
+    auto gen = [&](int i, int &val) -> bool {
+        val = P.cd[i + 1] - P.cd[i];
+        return true;
+    };
+    const double delta = median_int(gen, P.m - 1, P.m - 1, 0, 1 << 20);
+    const double adj = rint((double)(p.peek_size * 16) / delta);
+    if (adj > (double)p.peek_size) {
+        P.peek = adj > (double)CCDGPU_MAX_PEEK ? CCDGPU_MAX_PEEK : (int)adj;
+        P.chg = P.A->thr_table[P.peek];
+    }
+}
+
+// ------------------------------------------------------------------ Tmask (models/tmask.py + robust_fit.py)
+// Cholesky solve of an n x n SPD system (n <= 5), redundantly in every lane (uniform result).
+__device__ bool chol5(double (&a)[5][5], int n) {
+    for (int j = 0; j < n; ++j) {
+        double d = a[j][j];
+        for (int k = 0; k < j; ++k) d -= a[j][k] * a[j][k];
+        if (!(d > 0.0)) return false;
+        d = sqrt(d);
+        a[j][j] = d;
+        for (int i = j + 1; i < n; ++i) {
+            double s = a[i][j];
+            for (int k = 0; k < j; ++k) s -= a[i][k] * a[j][k];
+            a[i][j] = s / d;
+        }
+    }
+    return true;
+}
+__device__ void chol_solve(const double (&c)[5][5], int n, const double *b, double *x) {
+    double z[5];
+    for (int i = 0; i < n; ++i) {
+        double s = b[i];
+        for (int k = 0; k < i; ++k) s -= c[i][k] * z[k];
+        z[i] = s / c[i][i];
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        double s = z[i];
+        for (int k = i + 1; k < n; ++k) s -= c[k][i] * x[k];
+        x[i] = s / c[i][i];
+    }
+}
+
+// weighted normal equations sum_i w_i x_i x_i^T, sum_i w_i x_i y_i over the window (lane = obs).
+// x rows: [c1, s1, (cos oc t, sin oc t), 1]; weights from wv (nullptr = 1).
+__device__ bool tm_solve(const Px &P, int a, int nw, int ncol, const double *xoc, const double *xos,
+                         int band, const double *wv, double *coef) {
+    const int l = lane();
+    double acc[20];
+#pragma unroll
+    for (int e = 0; e < 20; ++e) acc[e] = 0.0;
+    for (int t0 = 0; t0 < nw; t0 += W) {
+        const int i = t0 + l;
+        if (i < nw) {
+            const double *bs = P.basis + (size_t)P.ci[a + i] * CCD_BASIS_STRIDE;
+            double x[5];
+            x[0] = bs[1];
+            x[1] = bs[2];
+            if (ncol == 5) { x[2] = xoc[i]; x[3] = xos[i]; x[4] = 1.0; }
+            else { x[2] = 1.0; x[3] = 0.0; x[4] = 0.0; }
+            const double wt = wv ? wv[i] : 1.0;
+            const double y = cvalf(P, band, a + i);
+            int e = 0;
+#pragma unroll
+            for (int r = 0; r < 5; ++r) {
+#pragma unroll
+                for (int c = 0; c <= r; ++c) acc[e++] += wt * x[r] * x[c];
+            }
+#pragma unroll
+            for (int r = 0; r < 5; ++r) acc[15 + r] += wt * x[r] * y;
+        }
+    }
+    double A[5][5], rhs[5];
+    int e = 0;
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+#pragma unroll
+        for (int c = 0; c <= r; ++c) {
+            const double v = wsum(acc[e++]);
+            A[r][c] = v;
+            A[c][r] = v;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 5; ++r) rhs[r] = wsum(acc[15 + r]);
+    if (!chol5(A, ncol)) {
+        for (int r = 0; r < 5; ++r) coef[r] = 0.0;
+        return false;
+    }
+    chol_solve(A, ncol, rhs, coef);
+    for (int r = ncol; r < 5; ++r) coef[r] = 0.0;
+    return true;
+}
+
+__device__ __forceinline__ double tm_pred(const Px &P, int j, int ncol, double xc, double xs, const double *coef) {
+    const double *bs = P.basis + (size_t)P.ci[j] * CCD_BASIS_STRIDE;
+    double pr = bs[1] * coef[0] + bs[2] * coef[1];
+    if (ncol == 5) pr += xc * coef[2] + xs * coef[3] + coef[4];
+    else pr += coef[2];
+    return pr;
+}
+
+// Returns the outlier count; outlier flags in L->tflag (bit i = window observation i).
+__device__ int tmask(Px &P, int a, int b) {
+    const ccdgpu_params &p = P.A->p;
+    Lds *L = P.L;
+    const int l = lane();
+    const int nw = b - a;
+    const double w = 2.0 * M_PI / p.avg_days_yr;
+    const double oc = w / ceil(((double)P.cd[b - 1] - (double)P.cd[a]) / p.avg_days_yr);
+    const int ncol = (oc == w) ? 3 : 5;
+    double *xoc = P.fs, *xos = P.fs + P.n, *adj = P.fs + 2 * P.n, *absr = P.fs + 3 * P.n,
+           *wt = P.fs + 4 * P.n;
+    // observation-cycle harmonics and flags
+    for (int t0 = 0; t0 < nw; t0 += W) {
+        const int i = t0 + l;
+        if (i < nw && ncol == 5) {
+            const double t = (double)P.cd[a + i];
+            double sv, cv;
+            sincos(oc * t, &sv, &cv);
+            xoc[i] = cv;
+            xos[i] = sv;
+        }
+    }
+    for (int i = l; i < (nw + 31) / 32; i += W) L->tflag[i] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    wsync();
+    // leverage from the unweighted normal matrix (robust_fit.RLM: h = diag(X (X'X)^-1 X'))
+    double G0[5][5];
+    {
+        double acc[15];
+#pragma unroll
+        for (int e = 0; e < 15; ++e) acc[e] = 0.0;
+        for (int t0 = 0; t0 < nw; t0 += W) {
+            const int i = t0 + l;
+            if (i < nw) {
+                const double *bs = P.basis + (size_t)P.ci[a + i] * CCD_BASIS_STRIDE;
+                double x[5] = {bs[1], bs[2], ncol == 5 ? xoc[i] : 1.0, ncol == 5 ? xos[i] : 0.0,
+                               ncol == 5 ? 1.0 : 0.0};
+                int e = 0;
+#pragma unroll
+                for (int r = 0; r < 5; ++r)
+#pragma unroll
+                    for (int c = 0; c <= r; ++c) acc[e++] += x[r] * x[c];
+            }
+        }
+        int e = 0;
+#pragma unroll
+        for (int r = 0; r < 5; ++r)
+#pragma unroll
+            for (int c = 0; c <= r; ++c) {
+                const double v = wsum(acc[e++]);
+                G0[r][c] = v;
+                G0[c][r] = v;
+            }
+        const bool ok = chol5(G0, ncol);
+        for (int t0 = 0; t0 < nw; t0 += W) {
+            const int i = t0 + l;
+            if (i < nw) {
+                const double *bs = P.basis + (size_t)P.ci[a + i] * CCD_BASIS_STRIDE;
+                double x[5] = {bs[1], bs[2], ncol == 5 ? xoc[i] : 1.0, ncol == 5 ? xos[i] : 0.0, 1.0};
+                double h = 0.9999;
+                if (ok) {
+                    double z[5], hh = 0.0;
+                    for (int r = 0; r < ncol; ++r) {
+                        double s = x[r];
+                        for (int k = 0; k < r; ++k) s -= G0[r][k] * z[k];
+                        z[r] = s / G0[r][r];
+                        hh += z[r] * z[r];
+                    }
+                    h = hh < 0.9999 ? hh : 0.9999;
+                }
+                adj[i] = 1.0 / sqrt(1.0 - h);
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    wsync();
+    for (int band = 0; band < NB; ++band) {
+        if (!((p.tmask_bands >> band) & 1u)) continue;
+        // y statistics (np.std, population)
+        double sy = 0.0;
+        for (int t0 = 0; t0 < nw; t0 += W)
+            if (t0 + l < nw) sy += cvalf(P, band, a + t0 + l);
+        const double ym = wsum(sy) / nw;
+        double sv = 0.0;
+        for (int t0 = 0; t0 < nw; t0 += W)
+            if (t0 + l < nw) {
+                const double d = cvalf(P, band, a + t0 + l) - ym;
+                sv += d * d;
+            }
+        const double ystd = sqrt(wsum(sv) / nw);
+        double coef[5], coef0[5];
+        tm_solve(P, a, nw, ncol, xoc, xos, band, nullptr, coef);
+        int iteration = 1;
+        bool converged = false;
+        while (!converged && iteration < 5) {
+#pragma unroll
+            for (int r = 0; r < 5; ++r) coef0[r] = coef[r];
+            for (int t0 = 0; t0 < nw; t0 += W) {
+                const int i = t0 + l;
+                if (i < nw) {
+                    const double r = (cvalf(P, band, a + i) -
+                                      tm_pred(P, a + i, ncol, ncol == 5 ? xoc[i] : 0.0, ncol == 5 ? xos[i] : 0.0, coef0)) *
+                                     adj[i];
+                    wt[i] = r;  // signed, adjusted residual
+                    absr[i] = fabs(r);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            wsync();
+            // mad = median(sort(|r|)[4:]) / 0.6745
+            const int c = nw - 4;
+            double med;
+            if (c & 1) med = kth_nonneg(absr, nw, 4 + c / 2);
+            else med = (kth_nonneg(absr, nw, 4 + c / 2 - 1) + kth_nonneg(absr, nw, 4 + c / 2)) / 2.0;
+            const double mad = med / 0.6745;
+            const double floor_ = 2.220446049250313e-16 * ystd;
+            const double scale = mad > floor_ ? mad : floor_;
+            for (int t0 = 0; t0 < nw; t0 += W) {
+                const int i = t0 + l;
+                if (i < nw) {
+                    const double u = wt[i] / scale;
+                    const double q = u / 4.685;
+                    const double om = 1.0 - q * q;
+                    wt[i] = fabs(u) < 4.685 ? om * om : 0.0;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            wsync();
+            tm_solve(P, a, nw, ncol, xoc, xos, band, wt, coef);
+            iteration += 1;
+            converged = true;
+#pragma unroll
+            for (int r = 0; r < 5; ++r)
+                if (coef[r] - coef0[r] > 1e-8) converged = false;
+        }
+        const double thr = L->vario[band] * p.t_const;
+        for (int t0 = 0; t0 < nw; t0 += W) {
+            const int i = t0 + l;
+            bool out = false;
+            if (i < nw) {
+                const double pr = tm_pred(P, a + i, ncol, ncol == 5 ? xoc[i] : 0.0, ncol == 5 ? xos[i] : 0.0, coef) + 0.0;
+                out = fabs(pr - cvalf(P, band, a + i)) > thr;
+            }
+            const unsigned long long bm = bal(out);
+            if (l == 0) {
+                L->tflag[t0 >> 5] |= (unsigned)bm;
+                if (t0 + 32 < nw) L->tflag[(t0 >> 5) + 1] |= (unsigned)(bm >> 32);
+            }
+        }
+        wsync();
+    }
+    int cnt = 0;
+    for (int i = l; i < (nw + 31) / 32; i += W) cnt += __popc(L->tflag[i]);
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+    wsync();
+    return cnt;
+}
+
+__device__ __forceinline__ bool tflag_at(const Lds *L, int i) { return (L->tflag[i >> 5] >> (i & 31)) & 1u; }
+
+// ------------------------------------------------------------------ change.py
+__device__ __forceinline__ int num_coefs(const ccdgpu_params &p, int n) {
+    const double span = (double)n / p.num_obs_factor;
+    if (span < p.coef_mid) return p.coef_min;
+    if (span < p.coef_max) return p.coef_mid;
+    return p.coef_max;
+}
+
+__device__ bool stable(const Px &P, int a, int b) {
+    const ccdgpu_params &p = P.A->p;
+    const Lds *L = P.L;
+    const int l = lane();
+    double v2 = 0.0;
+    if (l < NB && ((p.detection_bands >> l) & 1u)) {
+        const double rm = L->rmse[l];
+        const double vr = L->vario[l];
+        const double rn = rm > vr ? rm : vr;
+        const double slope = L->coef[l][0] * ((double)P.cd[b - 1] - (double)P.cd[a]);
+        const double v = (fabs(slope) + fabs(resid_at(P, l, a)) + fabs(resid_at(P, l, b - 1))) / rn;
+        v2 = v * v;
+    }
+    return sqrt(wsum(v2)) < P.chg;
+}
+
+__device__ bool initialize(Px &P, int &wa, int &wb) {
+    const ccdgpu_params &p = P.A->p;
+    const Lds *L = P.L;
+    const int l = lane();
+    int a = wa, b = wb;
+    bool ok = false;
+    while (b + p.meow_size < P.m) {
+        if (P.cd[b - 1] - P.cd[a] < p.day_delta) { b += 1; continue; }
+        const int cnt = tmask(P, a, b);
+        const int nw = b - a;
+        if (cnt == nw) { b += 1; continue; }
+        // first / last kept observation of the window
+        int first = 1 << 30, last = -1;
+        for (int t0 = 0; t0 < nw; t0 += W) {
+            const int i = t0 + l;
+            const bool kept = i < nw && !tflag_at(L, i);
+            const unsigned long long km = bal(kept);
+            if (km) {
+                const int f = t0 + __ffsll((long long)km) - 1;
+                const int la = t0 + 63 - __clzll(km);
+                first = f < first ? f : first;
+                last = la;
+            }
+        }
+        if (P.cd[a + last] - P.cd[a + first] < p.day_delta || nw - cnt < p.meow_size) { b += 1; continue; }
+        if (cnt) {
+            const int aa = a, bb = b;
+            compact_drop(P, a, [&](int j) { return j < bb && tflag_at(L, j - aa); });
+            b -= cnt;
+        }
+        fit_models(P, a, b, 4);
+        if (!stable(P, a, b)) { a += 1; b += 1; continue; }
+        ok = true;
+        break;
+    }
+    wa = a;
+    wb = b;
+    return ok;
+}
+
+// change magnitude of the lane's peek residuals (only detection bands)
+__device__ __forceinline__ double magnitude(const Px &P, const double (&r)[NB], const double *comp) {
+    const ccdgpu_params &p = P.A->p;
+    double s = 0.0;
+#pragma unroll
+    for (int band = 0; band < NB; ++band) {
+        if (!((p.detection_bands >> band) & 1u)) continue;
+        const double vr = P.L->vario[band];
+        const double cr = comp[band];
+        const double rm = (vr != vr || cr != cr) ? __builtin_nan("") : (vr > cr ? vr : cr);
+        const double v = r[band] / rm;
+        s += v * v;
+    }
+    return s;
+}
+
+__device__ void lookback(Px &P, int &wa, int &wb, int prev) {
+    const ccdgpu_params &p = P.A->p;
+    const int l = lane();
+    int a = wa, b = wb;
+    double comp[NB];
+#pragma unroll
+    for (int band = 0; band < NB; ++band) comp[band] = P.L->rmse[band];
+    while (a > prev) {
+        int lo;
+        if (a - prev > P.peek) lo = a - P.peek + 1;
+        else if (a - P.peek <= 0) lo = 0;
+        else lo = prev;
+        const int k = a - lo;
+        double r[NB];
+        double mag = 0.0;
+        if (l < k) {
+#pragma unroll
+            for (int band = 0; band < NB; ++band) r[band] = resid_at(P, band, a - 1 - l);
+            mag = magnitude(P, r, comp);
+        }
+        const bool change = bal(l < k && !(mag > P.chg)) == 0ull;
+        if (change) break;
+        const double m0 = __shfl(mag, 0);
+        if (m0 > p.outlier_threshold) {
+            const int rm = a - 1;
+            compact_drop(P, rm, [&](int j) { return j == rm; });
+            a -= 1;
+            b -= 1;
+            continue;
+        }
+        a -= 1;
+    }
+    wa = a;
+    wb = b;
+}
+
+// median over lanes [0, k) of v (per band), rank counting with shuffles
+__device__ double lane_median(double v, int k) {
+    const int l = lane();
+    int rank = 0;
+    for (int i = 0; i < k; ++i) {
+        const double u = __shfl(v, i);
+        rank += (u < v || (u == v && i < l)) ? 1 : 0;
+    }
+    const int t1 = (k - 1) / 2, t2 = k / 2;
+    const unsigned long long m1 = bal(l < k && rank == t1);
+    const unsigned long long m2 = bal(l < k && rank == t2);
+    const double a = __shfl(v, __ffsll((long long)m1) - 1);
+    const double b = __shfl(v, __ffsll((long long)m2) - 1);
+    return (k & 1) ? a : (a + b) / 2.0;
+}
+
+__device__ void lookforward(Px &P, int &wa, int &wb) {
+    const ccdgpu_params &p = P.A->p;
+    const int l = lane();
+    int a = wa, b = wb;
+    int fa = a, fb = b;
+    bool have = false;
+    double change = 0.0;
+    int nc = p.coef_min;
+    double fit_span = (double)P.cd[b - 1] - (double)P.cd[a];
+    double comp[NB];
+    double r[NB] = {0, 0, 0, 0, 0, 0, 0};
+    int peek_start = b;
+    while (b + P.peek < P.m || !have) {
+        nc = num_coefs(p, b - a);
+        peek_start = b;
+        const int k = P.peek;
+        const double model_span = (double)P.cd[b - 1] - (double)P.cd[a];
+        if (!have || b - a < 24) {
+            fa = a;
+            fb = b;
+            fit_span = (double)P.cd[b - 1] - (double)P.cd[a];
+            fit_models(P, fa, fb, nc);
+            have = true;
+#pragma unroll
+            for (int band = 0; band < NB; ++band) comp[band] = P.L->rmse[band];
+        } else {
+            if (model_span >= 1.33 * fit_span) {
+                fa = a;
+                fb = b;
+                fit_span = (double)P.cd[b - 1] - (double)P.cd[a];
+                fit_models(P, fa, fb, nc);
+            }
+            // find_closest_doy(period, peek.stop - 1, fit_window, 24) -> comparison rmse
+            const int nf = fb - fa;
+            const int ref = P.cd[b + k - 1];
+            auto key4 = [&](int i) -> int {
+                const double d = (double)(P.cd[fa + i] - ref);
+                const double kk = fabs(rint(d / 365.25) * 365.25 - d);
+                return (int)(kk * 4.0 + 0.5);
+            };
+            int K = 1 << 20, need = 0;
+            if (nf > 24) {
+                auto gen = [&](int i, int &v) -> bool { v = key4(i); return true; };
+                K = kth_int(gen, nf, 23, 0, 1461);
+                int less = 0;
+                for (int t0 = 0; t0 < nf; t0 += W) {
+                    const int i = t0 + l;
+                    less += popc(bal(i < nf && key4(i) < K));
+                }
+                need = 24 - less;
+            }
+            double ss[NB] = {0, 0, 0, 0, 0, 0, 0};
+            int taken_eq = 0;
+            for (int t0 = 0; t0 < nf; t0 += W) {
+                const int i = t0 + l;
+                int kv = 1 << 21;
+                if (i < nf) kv = key4(i);
+                const unsigned long long eq = bal(i < nf && kv == K);
+                const bool sel = i < nf && (kv < K || (kv == K && taken_eq + below(eq) < need));
+                taken_eq += popc(eq);
+                if (sel) {
+#pragma unroll
+                    for (int band = 0; band < NB; ++band) {
+                        const double e = resid_at(P, band, fa + i);
+                        ss[band] += e * e;
+                    }
+                }
+            }
+#pragma unroll
+            for (int band = 0; band < NB; ++band) comp[band] = sqrt(wsum(ss[band])) / 4.0;
+        }
+        double mag = 0.0;
+        if (l < k) {
+#pragma unroll
+            for (int band = 0; band < NB; ++band) r[band] = resid_at(P, band, b + l);
+            mag = magnitude(P, r, comp);
+        }
+        const bool chg = bal(l < k && !(mag > P.chg)) == 0ull;
+        if (chg) {
+            change = 1.0;
+            break;
+        }
+        const double m0 = __shfl(mag, 0);
+        if (m0 > p.outlier_threshold) {
+            const int rm = b;
+            compact_drop(P, rm, [&](int j) { return j == rm; });
+            continue;
+        }
+        b += 1;
+    }
+    // magnitudes: median over the last peek residuals, per band (lane b gets band b)
+    double mag_lane = 0.0;
+#pragma unroll
+    for (int band = 0; band < NB; ++band) {
+        const double md = lane_median(r[band], P.peek);
+        if (l == band) mag_lane = md;
+    }
+    emit(P, P.cd[a], P.cd[b - 1], P.cd[peek_start], b - a, change, nc, mag_lane);
+    wa = a;
+    wb = b;
+}
+
+__device__ void standard_procedure(Px &P) {
+    const ccdgpu_params &p = P.A->p;
+    const int meow = p.meow_size;
+    variogram(P);
+    adjust_peek(P);
+    int a = 0, b = meow, prev = 0, nres = 0;
+    bool start = true;
+    while (b <= P.m - meow) {
+        if (nres > 0) start = false;
+        if (!initialize(P, a, b)) break;
+        if (a > prev) lookback(P, a, b, prev);
+        if (a - prev > P.peek && start) {
+            catch_(P, prev, a, p.curve_qa_start);
+            nres++;
+            start = false;
+        }
+        if (b + P.peek > P.m) break;
+        lookforward(P, a, b);
+        nres++;
+        prev = b;
+        a = b;
+        b = b + meow;
+    }
+    if (prev + P.peek < P.m) catch_(P, prev, P.m, p.curve_qa_end);
+}
+
+// ------------------------------------------------------------------ qa.py filters + compaction
+// Returns the procedure, or -1 for an unsupported QA value.
+__device__ int px_setup(Px &P, int chip, int pix) {
+    const CcdDetectArgs &A = *P.A;
+    const ccdgpu_params &p = A.p;
+    Lds *L = P.L;
+    const int l = lane();
+    const int n = P.n;
+    const int32_t *order = A.order + (size_t)chip * n;
+    const uint16_t *qa = A.qa + ((size_t)chip * A.n_pix + pix) * n;
+    const size_t bstride = (size_t)A.n_pix * n;
+    const int16_t *sp = A.spectra + (size_t)chip * NB * bstride + (size_t)pix * n;
+    int c_clear = 0, c_water = 0, c_snow = 0, c_cloud = 0, c_fill = 0;
+    bool bad = false;
+    for (int base = 0; base < n; base += W) {
+        const int i = base + l;
+        int cls = -2;
+        if (i < n) {
+            const unsigned q = qa[order[i]];
+            cls = p.qa_bitpacked ? qabitval(p, q) : (int)q;
+        }
+        c_clear += popc(bal(i < n && cls == p.qa_clear));
+        c_water += popc(bal(i < n && cls == p.qa_water));
+        c_snow += popc(bal(i < n && cls == p.qa_snow));
+        c_cloud += popc(bal(i < n && cls == p.qa_cloud));
+        c_fill += popc(bal(i < n && cls == p.qa_fill));
+        if (bal(i < n && cls < 0)) bad = true;
+    }
+    if (bad) return -1;
+    const int total = n - c_fill;
+    const int cw = c_clear + c_water;
+    if (l == 0) {
+        double *pr = A.probs + 3 * (size_t)P.gpix;
+        pr[0] = (double)c_cloud / (double)total;
+        pr[1] = (double)c_snow / ((double)(cw + c_snow) + 0.01);
+        pr[2] = (double)c_water / ((double)(cw + c_snow) + 0.01);
+    }
+    int proc;
+    if (!((double)cw / (double)total >= p.clear_pct_threshold))
+        proc = ((double)c_snow / ((double)(cw + c_snow) + 0.01) >= p.snow_pct_threshold)
+                   ? CCDGPU_PROC_PERMANENT_SNOW : CCDGPU_PROC_INSUFFICIENT_CLEAR;
+    else
+        proc = CCDGPU_PROC_STANDARD;
+    const bool conv = proc == CCDGPU_PROC_STANDARD && p.kelvin_to_celsius;
+    for (int i = l; i < A.mask_words; i += W) L->mask[i] = 0u;
+    int m = 0;
+    int carry = -1;  // date of the last kept observation (ordinals are >= 1)
+    for (int base = 0; base < n; base += W) {
+        const int i = base + l;
+        const bool valid = i < n;
+        int cls = -2, d = 0;
+        int16_t v[NB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) v[b] = 0;
+        if (valid) {
+            const int o = order[i];
+            const unsigned q = qa[o];
+            cls = p.qa_bitpacked ? qabitval(p, q) : (int)q;
+#pragma unroll
+            for (int b = 0; b < NB; ++b) v[b] = sp[(size_t)b * bstride + o];
+            if (conv) v[6] = (int16_t)((int)v[6] * 10 - 27315);
+            d = (int)P.sd[i];
+        }
+        const bool cwi = cls == p.qa_clear || cls == p.qa_water;
+        const bool th = v[6] > p.thermal_min && v[6] < p.thermal_max;
+        bool sat = true;
+#pragma unroll
+        for (int b = 0; b < 6; ++b) sat = sat && v[b] > 0 && v[b] < 10000;
+        bool keep = valid && cwi && th && sat;
+        if (proc == CCDGPU_PROC_PERMANENT_SNOW) keep = keep || (valid && cls == p.qa_snow);
+        const unsigned long long km = bal(keep);
+        const unsigned long long lower = l ? (km & ((1ull << l) - 1ull)) : 0ull;
+        const int pl = lower ? 63 - __clzll(lower) : l;
+        const int pd = __shfl(d, pl);
+        const int prevd = lower ? pd : carry;
+        const bool keep2 = keep && d != prevd;
+        if (km) carry = __shfl(d, 63 - __clzll(km));
+        const unsigned long long k2 = bal(keep2);
+        if (keep2) {
+            const int pos = m + below(k2);
+            P.cd[pos] = d;
+            P.ci[pos] = (uint16_t)i;
+#pragma unroll
+            for (int b = 0; b < NB; ++b) P.cv[(size_t)b * n + pos] = v[b];
+        }
+        if (l == 0) {
+            L->mask[base >> 5] = (unsigned)k2;
+            if (base + 32 < n) L->mask[(base >> 5) + 1] = (unsigned)(k2 >> 32);
+        }
+        m += popc(k2);
+    }
+    P.m = m;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    wsync();
+    if (proc == CCDGPU_PROC_INSUFFICIENT_CLEAR && m > 0) {
+        const int16_t *g = P.cv + (size_t)1 * n;
+        auto gen = [&](int i, int &val) -> bool { val = g[i]; return true; };
+        const double med = median_int(gen, m, m, -32768, 32767) + (double)p.median_green_filter;
+        compact_drop(P, 0, [&](int j) { return !((double)g[j] < med); });
+    }
+    return proc;
+}
+
+__global__ __launch_bounds__(64) void ccd_detect(const CcdDetectArgs *__restrict__ Ap) {
+    __shared__ Lds lds;
+    const CcdDetectArgs &A = *Ap;
+    const int l = lane();
+    const int slot = blockIdx.x;
+    Px P;
+    P.A = &A;
+    P.L = &lds;
+    P.n = A.n_obs;
+    P.cd = A.s_date + (size_t)slot * A.n_obs;
+    P.ci = A.s_idx + (size_t)slot * A.n_obs;
+    P.cv = A.s_val + (size_t)slot * NB * A.n_obs;
+    P.fs = A.s_f64 + (size_t)slot * 5 * A.n_obs;
+    P.fits = 0;
+    P.sweeps = 0;
+    for (;;) {
+        unsigned long long job = 0;
+        if (l == 0) job = atomicAdd(&A.counters[0], 1ull);
+        job = __shfl((unsigned long long)job, 0);
+        if (job >= (unsigned long long)A.total_pix) break;
+        const int chip = (int)(job / (unsigned long long)A.n_pix);
+        const int pix = (int)(job % (unsigned long long)A.n_pix);
+        P.gpix = (int64_t)job;
+        P.nseg = 0;
+        P.basis = A.basis + (size_t)chip * A.n_obs * CCD_BASIS_STRIDE;
+        P.sd = A.sdates + (size_t)chip * A.n_obs;
+        const int proc = px_setup(P, chip, pix);
+        if (proc < 0) {
+            if (l == 0) {
+                atomicMin(&A.counters[2], (unsigned long long)job);
+                A.procedure[job] = -1;
+                A.nseg[job] = 0;
+            }
+            for (int i = l; i < A.mask_words; i += W) A.mask_bits[(size_t)job * A.mask_words + i] = 0u;
+            continue;
+        }
+        if (proc == CCDGPU_PROC_STANDARD) {
+            standard_procedure(P);
+        } else if (P.m >= A.p.meow_size) {
+            fit_models(P, 0, P.m, A.p.coef_min);
+            emit(P, (int)P.sd[0], (int)P.sd[A.n_obs - 1], 0, P.m, 0.0,
+                 proc == CCDGPU_PROC_PERMANENT_SNOW ? A.p.curve_qa_persist_snow : A.p.curve_qa_insuf_clear, 0.0);
+        }
+        wsync();
+        for (int i = l; i < A.mask_words; i += W) A.mask_bits[(size_t)job * A.mask_words + i] = lds.mask[i];
+        if (l == 0) {
+            A.procedure[job] = proc;
+            A.nseg[job] = P.nseg;
+        }
+        wsync();
+    }
+    // instrumentation
+    unsigned long long sw = P.sweeps;
+    for (int o = 32; o > 0; o >>= 1) sw += __shfl_xor(sw, o);
+    if (l == 0) {
+        atomicAdd(&A.stats[0], P.fits);
+        atomicAdd(&A.stats[1], sw);
+    }
+}
+
+// ------------------------------------------------------------------ per-chip preparation
+// One 256-thread block per chip: stable rank of each date (ties by input position), sorted
+// dates, order, and the coefficient_matrix rows (w = 2 pi / avg_days_yr; cos/sin of w t, 2 w t,
+// 3 w t exactly as models/lasso.coefficient_matrix forms them).
+__global__ __launch_bounds__(256) void ccd_prep(const int64_t *dates, int n, double avg_days_yr,
+                                                int32_t *order, int64_t *sdates, double *basis) {
+    const int chip = blockIdx.x;
+    const int64_t *d = dates + (size_t)chip * n;
+    int32_t *ord = order + (size_t)chip * n;
+    int64_t *sd = sdates + (size_t)chip * n;
+    double *bs = basis + (size_t)chip * n * CCD_BASIS_STRIDE;
+    __shared__ int64_t sdl[CCDGPU_MAX_OBS];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) sdl[i] = d[i];
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int64_t di = sdl[i];
+        int rank = 0;
+        for (int j = 0; j < n; ++j) {
+            const int64_t dj = sdl[j];
+            rank += (dj < di || (dj == di && j < i)) ? 1 : 0;
+        }
+        ord[rank] = i;
+        sd[rank] = di;
+        const double w = 2.0 * M_PI / avg_days_yr;
+        const double w12 = w * (double)di;
+        const double w34 = 2.0 * w12;
+        const double w56 = 3.0 * w12;
+        double *r = bs + (size_t)rank * CCD_BASIS_STRIDE;
+        r[0] = (double)di;
+        r[1] = cos(w12);
+        r[2] = sin(w12);
+        r[3] = cos(w34);
+        r[4] = sin(w34);
+        r[5] = cos(w56);
+        r[6] = sin(w56);
+        r[7] = 0.0;
+    }
+}
+
+// Pool -> CSR: one wave per pooled segment, dwords copied lane-parallel.
+__global__ __launch_bounds__(256) void ccd_scatter(const ccdgpu_segment *pool, const int32_t *seq, int64_t n_pool,
+                                                   const int64_t *offsets, int n_pix_per_chip,
+                                                   ccdgpu_segment *out) {
+    const int64_t s = (int64_t)blockIdx.x * (blockDim.x / W) + threadIdx.x / W;
+    if (s >= n_pool) return;
+    const int l = threadIdx.x % W;
+    const int gp = pool[s].pixel;
+    const int64_t dst = offsets[gp] + seq[s];
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(pool + s);
+    uint32_t *dd = reinterpret_cast<uint32_t *>(out + dst);
+    constexpr int NW = (int)(sizeof(ccdgpu_segment) / 4);
+    constexpr int PIXW = (int)(offsetof(ccdgpu_segment, pixel) / 4);
+    for (int i = l; i < NW; i += W) dd[i] = (i == PIXW) ? (uint32_t)(gp % n_pix_per_chip) : src[i];
+}
+
+}  // namespace
+
+extern "C" int ccdk_prep(const int64_t *dates, int32_t n_chips, int32_t n_obs, double avg_days_yr,
+                         int32_t *order, int64_t *sdates, double *basis, void *stream) {
+    hipLaunchKernelGGL(ccd_prep, dim3(n_chips), dim3(256), 0, (hipStream_t)stream, dates, n_obs,
+                       avg_days_yr, order, sdates, basis);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int ccdk_detect(const CcdDetectArgs *dev_args, int32_t grid, void *stream) {
+    hipLaunchKernelGGL(ccd_detect, dim3(grid), dim3(64), 0, (hipStream_t)stream, dev_args);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int ccdk_scatter(const ccdgpu_segment *pool, const int32_t *pool_seq, int64_t n_pool,
+                            const int64_t *offsets, int32_t n_pix_per_chip, ccdgpu_segment *out,
+                            void *stream) {
+    if (n_pool <= 0) return 0;
+    const int per_block = 256 / W;
+    const int64_t blocks = (n_pool + per_block - 1) / per_block;
+    hipLaunchKernelGGL(ccd_scatter, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, pool,
+                       pool_seq, n_pool, offsets, n_pix_per_chip, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

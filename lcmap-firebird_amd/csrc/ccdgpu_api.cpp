@@ -1,0 +1,474 @@
+// ccdgpu_api.cpp -- host side of the C-ABI declared in include/ccdgpu.h.
+//
+// Owns device memory and one HIP stream per context.  A detection call = H2D of the chip stack
+// (band-major, observation-contiguous, exactly the layout the Python packer hands over), the
+// per-chip prep kernel, the persistent per-pixel detection kernel, an exclusive scan of the
+// per-pixel segment counts (hipCUB) and the pool->CSR scatter, then D2H of the CSR result.
+// Replaces the per-pixel ccd.detect call of ccdc/pyccd.py:168 (see include/ccdgpu.h).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/ccdgpu.h"
+#include "ccd_device.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                       \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return fail(CCDGPU_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
+    } while (0)
+
+template <class T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t cap = 0;  // elements
+    int ensure(size_t n) {
+        if (n <= cap && p) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        if (hipMalloc(&p, sizeof(T) * (n ? n : 1)) != hipSuccess) {
+            p = nullptr;
+            return fail(CCDGPU_ENOMEM, "hipMalloc failed (" + std::to_string(sizeof(T) * n) + " bytes)");
+        }
+        cap = n;
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+double chi2_5_cdf(double x) {
+    if (x <= 0) return 0.0;
+    return std::erf(std::sqrt(x / 2.0)) - std::sqrt(2.0 * x / M_PI) * std::exp(-x / 2.0) * (1.0 + x / 3.0);
+}
+
+// inverse chi-square(5) cdf (change.adjustchgthresh uses scipy chi2.ppf(pt_cg, 5))
+double chi2_5_ppf(double p) {
+    double lo = 0.0, hi = 400.0;
+    for (int i = 0; i < 200; ++i) {
+        const double mid = 0.5 * (lo + hi);
+        if (chi2_5_cdf(mid) < p) lo = mid;
+        else hi = mid;
+    }
+    return 0.5 * (lo + hi);
+}
+
+}  // namespace
+
+struct ccdgpu_ctx {
+    int device = 0;
+    int n_cu = 0;
+    int slots_per_cu = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // staged batch
+    bool staged = false, ran = false;
+    ccdgpu_params params{};
+    int32_t n_chips = 0, n_pix = 0, n_obs = 0, mask_words = 0, n_slots = 0;
+    int64_t total_pix = 0, pool_cap = 0, n_pool = 0;
+    DevBuf<int64_t> dates, sdates, offsets;
+    DevBuf<int16_t> spectra;
+    DevBuf<uint16_t> qa;
+    DevBuf<int32_t> order, procedure, nseg, pool_seq;
+    DevBuf<double> basis, probs, s_f64;
+    DevBuf<unsigned long long> counters, stats;
+    DevBuf<int32_t> s_date;
+    DevBuf<uint16_t> s_idx;
+    DevBuf<int16_t> s_val;
+    DevBuf<uint32_t> mask;
+    DevBuf<ccdgpu_segment> pool, csr;
+    DevBuf<CcdDetectArgs> args;
+    DevBuf<unsigned char> cub_tmp;
+    std::vector<int64_t> h_offsets;
+    ccdgpu_stats last{};
+    ~ccdgpu_ctx() {
+        for (auto *b : {&dates, &sdates, &offsets}) b->release();
+        spectra.release();
+        qa.release();
+        for (auto *b : {&order, &procedure, &nseg, &pool_seq, &s_date}) b->release();
+        for (auto *b : {&basis, &probs, &s_f64}) b->release();
+        counters.release();
+        stats.release();
+        s_idx.release();
+        s_val.release();
+        mask.release();
+        pool.release();
+        csr.release();
+        args.release();
+        cub_tmp.release();
+        for (auto &e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+extern "C" {
+
+const char *ccdgpu_version(void) { return "ccdgpu 0.1.0 (gfx950; lcmap-pyccd:2018.03.12.dev-ncompare.b2 semantics)"; }
+
+const char *ccdgpu_last_error(void) { return g_err.c_str(); }
+
+void ccdgpu_params_default(ccdgpu_params *p) {
+    std::memset(p, 0, sizeof(*p));
+    p->meow_size = 12;
+    p->peek_size = 6;
+    p->day_delta = 365;
+    p->coef_min = 4;
+    p->coef_mid = 6;
+    p->coef_max = 8;
+    p->num_obs_factor = 3;
+    p->detection_bands = 0x3E;
+    p->tmask_bands = 0x12;
+    p->lasso_max_iter = 1000;
+    p->thermal_min = -9320;
+    p->thermal_max = 7070;
+    p->median_green_filter = 400;
+    p->curve_qa_start = 14;
+    p->curve_qa_end = 24;
+    p->curve_qa_insuf_clear = 44;
+    p->curve_qa_persist_snow = 54;
+    p->qa_fill = 0;
+    p->qa_clear = 1;
+    p->qa_water = 2;
+    p->qa_shadow = 3;
+    p->qa_snow = 4;
+    p->qa_cloud = 5;
+    p->qa_cirrus1 = 8;
+    p->qa_cirrus2 = 9;
+    p->qa_occlusion = 10;
+    p->qa_bitpacked = 1;
+    p->adaptive_peek = 1;
+    p->rmse_dof = 0;
+    p->kelvin_to_celsius = 1;
+    p->avg_days_yr = 365.2425;
+    p->change_probability = 0.99;
+    p->change_threshold = 15.086272469388987;
+    p->outlier_threshold = 35.888186879610423;
+    p->t_const = 4.42;
+    p->lasso_alpha = 1.0;
+    p->lasso_tol = 1e-4;
+    p->clear_pct_threshold = 0.25;
+    p->snow_pct_threshold = 0.75;
+}
+
+int ccdgpu_device_count(int *count) {
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) {
+        *count = 0;
+        return fail(CCDGPU_EHIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+    }
+    *count = c;
+    return 0;
+}
+
+int ccdgpu_init(int device, ccdgpu_ctx **out) {
+    if (!out) return fail(CCDGPU_EINVAL, "ctx out pointer is NULL");
+    *out = nullptr;
+    int count = 0;
+    int rc = ccdgpu_device_count(&count);
+    if (rc) return rc;
+    if (device < 0 || device >= count)
+        return fail(CCDGPU_EINVAL, "device " + std::to_string(device) + " out of range (" + std::to_string(count) + " visible)");
+    HIPCHK(hipSetDevice(device));
+    auto *c = new ccdgpu_ctx();
+    c->device = device;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+        delete c;
+        return fail(CCDGPU_EHIP, "hipGetDeviceProperties failed");
+    }
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        std::string arch = prop.gcnArchName;
+        delete c;
+        return fail(CCDGPU_EHIP, "device " + std::to_string(device) + " is " + arch + ", libccdgpu is built for gfx950 only");
+    }
+    c->n_cu = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return fail(CCDGPU_EHIP, "hipStreamCreate failed");
+    }
+    for (auto &e : c->ev) (void)hipEventCreate(&e);
+    c->slots_per_cu = 16;
+    *out = c;
+    return 0;
+}
+
+int ccdgpu_destroy(ccdgpu_ctx *ctx) {
+    if (!ctx) return 0;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    delete ctx;
+    return 0;
+}
+
+int ccdgpu_synchronize(ccdgpu_ctx *ctx) {
+    if (!ctx) return fail(CCDGPU_EINVAL, "NULL ctx");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipDeviceSynchronize());
+    return 0;
+}
+
+static int check_params(const ccdgpu_params *p, int32_t n_pix, int32_t n_obs) {
+    if (!p) return fail(CCDGPU_EINVAL, "params is NULL");
+    if (n_pix <= 0) return fail(CCDGPU_EINVAL, "n_pix must be > 0");
+    if (n_obs <= 0 || n_obs > CCDGPU_MAX_OBS)
+        return fail(CCDGPU_EINVAL, "n_obs must be in [1, " + std::to_string(CCDGPU_MAX_OBS) + "]");
+    if (p->peek_size < 1 || p->peek_size > CCDGPU_MAX_PEEK)
+        return fail(CCDGPU_EINVAL, "peek_size must be in [1, " + std::to_string(CCDGPU_MAX_PEEK) + "]");
+    if (p->meow_size < 5) return fail(CCDGPU_EINVAL, "meow_size must be >= 5 (Tmask needs > 4 observations)");
+    if (p->coef_min != 4 && p->coef_min != 6 && p->coef_min != 8)
+        return fail(CCDGPU_EINVAL, "coefficient counts must be 4, 6 or 8");
+    if ((p->coef_mid != 4 && p->coef_mid != 6 && p->coef_mid != 8) || (p->coef_max != 4 && p->coef_max != 6 && p->coef_max != 8))
+        return fail(CCDGPU_EINVAL, "coefficient counts must be 4, 6 or 8");
+    if (p->lasso_max_iter < 1) return fail(CCDGPU_EINVAL, "lasso_max_iter must be >= 1");
+    if ((p->detection_bands & ~0x7Fu) || (p->tmask_bands & ~0x7Fu))
+        return fail(CCDGPU_EINVAL, "band masks must only use bits 0..6");
+    return 0;
+}
+
+int ccdgpu_stage(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_chips, int32_t n_pix, int32_t n_obs,
+                 const int64_t *dates, const int16_t *spectra, const uint16_t *qa) {
+    if (!c) return fail(CCDGPU_EINVAL, "NULL ctx");
+    if (n_chips <= 0) return fail(CCDGPU_EINVAL, "n_chips must be > 0");
+    int rc = check_params(params, n_pix, n_obs);
+    if (rc) return rc;
+    if (!dates || !spectra || !qa) return fail(CCDGPU_EINVAL, "NULL input buffer");
+    HIPCHK(hipSetDevice(c->device));
+    c->params = *params;
+    c->n_chips = n_chips;
+    c->n_pix = n_pix;
+    c->n_obs = n_obs;
+    c->mask_words = (n_obs + 31) / 32;
+    c->total_pix = (int64_t)n_chips * n_pix;
+    const size_t nc = (size_t)n_chips, np = (size_t)n_pix, no = (size_t)n_obs;
+    if ((rc = c->dates.ensure(nc * no)) || (rc = c->spectra.ensure(nc * 7 * np * no)) ||
+        (rc = c->qa.ensure(nc * np * no)) || (rc = c->order.ensure(nc * no)) ||
+        (rc = c->sdates.ensure(nc * no)) || (rc = c->basis.ensure(nc * no * CCD_BASIS_STRIDE)) ||
+        (rc = c->procedure.ensure(c->total_pix)) || (rc = c->nseg.ensure(c->total_pix)) ||
+        (rc = c->probs.ensure(3 * c->total_pix)) || (rc = c->offsets.ensure(c->total_pix + 1)) ||
+        (rc = c->mask.ensure((size_t)c->total_pix * c->mask_words)) || (rc = c->counters.ensure(8)) ||
+        (rc = c->stats.ensure(8)) || (rc = c->args.ensure(1)))
+        return rc;
+    c->n_slots = (int32_t)std::min<int64_t>(c->total_pix, (int64_t)c->n_cu * c->slots_per_cu);
+    const size_t ns = (size_t)c->n_slots;
+    if ((rc = c->s_date.ensure(ns * no)) || (rc = c->s_idx.ensure(ns * no)) || (rc = c->s_val.ensure(ns * 7 * no)) ||
+        (rc = c->s_f64.ensure(ns * 5 * no)))
+        return rc;
+    if (c->pool_cap < c->total_pix * 8) c->pool_cap = c->total_pix * 8;
+    if ((rc = c->pool.ensure(c->pool_cap)) || (rc = c->pool_seq.ensure(c->pool_cap))) return rc;
+    HIPCHK(hipMemcpyAsync(c->dates.p, dates, sizeof(int64_t) * nc * no, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->spectra.p, spectra, sizeof(int16_t) * nc * 7 * np * no, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->qa.p, qa, sizeof(uint16_t) * nc * np * no, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->staged = true;
+    c->ran = false;
+    return 0;
+}
+
+int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
+    if (!c || !c->staged) return fail(CCDGPU_EINVAL, "nothing staged");
+    HIPCHK(hipSetDevice(c->device));
+    const ccdgpu_params &p = c->params;
+    CcdDetectArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.p = p;
+    a.n_chips = c->n_chips;
+    a.n_pix = c->n_pix;
+    a.n_obs = c->n_obs;
+    a.mask_words = c->mask_words;
+    a.n_slots = c->n_slots;
+    a.total_pix = c->total_pix;
+    a.spectra = c->spectra.p;
+    a.qa = c->qa.p;
+    a.order = c->order.p;
+    a.sdates = c->sdates.p;
+    a.basis = c->basis.p;
+    a.counters = c->counters.p;
+    a.s_date = c->s_date.p;
+    a.s_idx = c->s_idx.p;
+    a.s_val = c->s_val.p;
+    a.s_f64 = c->s_f64.p;
+    a.mask_bits = c->mask.p;
+    a.procedure = c->procedure.p;
+    a.probs = c->probs.p;
+    a.nseg = c->nseg.p;
+    a.stats = c->stats.p;
+    for (int k = 0; k <= CCDGPU_MAX_PEEK; ++k) {
+        if (k <= p.peek_size) a.thr_table[k] = p.change_threshold;
+        else a.thr_table[k] = chi2_5_ppf(1.0 - std::pow(1.0 - p.change_probability, (double)p.peek_size / k));
+    }
+    for (int attempt = 0; attempt < 4; ++attempt) {
+        a.pool = c->pool.p;
+        a.pool_seq = c->pool_seq.p;
+        a.pool_cap = c->pool_cap;
+        unsigned long long init[8] = {0ull, 0ull, ~0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
+        HIPCHK(hipMemcpyAsync(c->counters.p, init, sizeof(init), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemsetAsync(c->stats.p, 0, sizeof(unsigned long long) * 8, c->stream));
+        HIPCHK(hipMemcpyAsync(c->args.p, &a, sizeof(a), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipEventRecord(c->ev[0], c->stream));
+        if (ccdk_prep(c->dates.p, c->n_chips, c->n_obs, p.avg_days_yr, c->order.p, c->sdates.p, c->basis.p, c->stream))
+            return fail(CCDGPU_EHIP, std::string("prep launch: ") + hipGetErrorString(hipGetLastError()));
+        HIPCHK(hipEventRecord(c->ev[1], c->stream));
+        if (ccdk_detect(c->args.p, c->n_slots, c->stream))
+            return fail(CCDGPU_EHIP, std::string("detect launch: ") + hipGetErrorString(hipGetLastError()));
+        HIPCHK(hipEventRecord(c->ev[2], c->stream));
+        unsigned long long h[8];
+        HIPCHK(hipMemcpyAsync(h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (h[3]) {  // pool overflow: grow and rerun
+            c->pool_cap = (int64_t)(h[1] + h[1] / 4 + 1024);
+            int rc;
+            if ((rc = c->pool.ensure(c->pool_cap)) || (rc = c->pool_seq.ensure(c->pool_cap))) return rc;
+            continue;
+        }
+        c->n_pool = (int64_t)h[1];
+        float ms_prep = 0.f, ms_det = 0.f;
+        (void)hipEventElapsedTime(&ms_prep, c->ev[0], c->ev[1]);
+        (void)hipEventElapsedTime(&ms_det, c->ev[1], c->ev[2]);
+        unsigned long long st[8];
+        HIPCHK(hipMemcpy(st, c->stats.p, sizeof(st), hipMemcpyDeviceToHost));
+        // CSR: exclusive scan of per-pixel counts, then scatter the pool
+        int rc;
+        if ((rc = c->csr.ensure(c->n_pool > 0 ? c->n_pool : 1))) return rc;
+        size_t tmp_bytes = 0;
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, c->nseg.p, c->offsets.p, (int)c->total_pix + 1, c->stream));
+        if ((rc = c->cub_tmp.ensure(tmp_bytes))) return rc;
+        // nseg has total_pix entries; the scan over total_pix+1 needs a trailing zero
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->cub_tmp.p, tmp_bytes, c->nseg.p, c->offsets.p, (int)c->total_pix, c->stream));
+        c->h_offsets.resize(c->total_pix + 1);
+        HIPCHK(hipMemcpyAsync(c->h_offsets.data(), c->offsets.p, sizeof(int64_t) * c->total_pix, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        c->h_offsets[c->total_pix] = c->n_pool;
+        if (ccdk_scatter(c->pool.p, c->pool_seq.p, c->n_pool, c->offsets.p, c->n_pix, c->csr.p, c->stream))
+            return fail(CCDGPU_EHIP, "scatter launch failed");
+        HIPCHK(hipEventRecord(c->ev[3], c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        c->last.detect_ms = ms_det;
+        c->last.prep_ms = ms_prep;
+        c->last.pixels = c->total_pix;
+        c->last.segments = c->n_pool;
+        c->last.lasso_fits = (int64_t)st[0];
+        c->last.cd_sweeps = (int64_t)st[1];
+        c->last.flops = (int64_t)st[2];
+        const int64_t in_bytes = c->total_pix * (int64_t)c->n_obs * 16 + (int64_t)c->n_chips * c->n_obs * 8;
+        const int64_t out_bytes = c->n_pool * (int64_t)sizeof(ccdgpu_segment) + c->total_pix * ((int64_t)c->mask_words * 4 + 4 + 24 + 4);
+        c->last.bytes = in_bytes + out_bytes;
+        if (kernel_seconds) *kernel_seconds = (ms_prep + ms_det) * 1e-3;
+        c->ran = true;
+        if (h[2] != ~0ull) {
+            g_err = "unsupported bit-packed QA value (pixel " + std::to_string(h[2]) + ")";
+            return CCDGPU_EQA;
+        }
+        return 0;
+    }
+    return fail(CCDGPU_EOVERFLOW, "segment pool kept overflowing");
+}
+
+int ccdgpu_last_stats(ccdgpu_ctx *c, ccdgpu_stats *s) {
+    if (!c || !s) return fail(CCDGPU_EINVAL, "NULL argument");
+    *s = c->last;
+    return 0;
+}
+
+static int fetch_chip(ccdgpu_ctx *c, int32_t chip, ccdgpu_result *out) {
+    std::memset(out, 0, sizeof(*out));
+    if (!c->ran) return fail(CCDGPU_EINVAL, "no completed run to fetch");
+    if (chip < 0 || chip >= c->n_chips) return fail(CCDGPU_EINVAL, "chip index out of range");
+    HIPCHK(hipSetDevice(c->device));
+    const int np = c->n_pix, no = c->n_obs;
+    const int64_t p0 = (int64_t)chip * np;
+    const int64_t s0 = c->h_offsets[p0], s1 = c->h_offsets[p0 + np];
+    out->n_pix = np;
+    out->n_obs = no;
+    out->n_seg = s1 - s0;
+    out->mask_words = c->mask_words;
+    out->error_pixel = -1;
+    out->seg_offsets = (int64_t *)std::malloc(sizeof(int64_t) * (np + 1));
+    out->segments = (ccdgpu_segment *)std::malloc(sizeof(ccdgpu_segment) * (size_t)(out->n_seg + 1));
+    out->mask_bits = (uint32_t *)std::malloc(sizeof(uint32_t) * (size_t)np * c->mask_words + 4);
+    out->procedure = (int32_t *)std::malloc(sizeof(int32_t) * np);
+    out->probs = (double *)std::malloc(sizeof(double) * 3 * np);
+    out->sorted_dates = (int64_t *)std::malloc(sizeof(int64_t) * no);
+    out->sort_index = (int32_t *)std::malloc(sizeof(int32_t) * no);
+    if (!out->seg_offsets || !out->segments || !out->mask_bits || !out->procedure || !out->probs ||
+        !out->sorted_dates || !out->sort_index) {
+        ccdgpu_result_free(out);
+        return fail(CCDGPU_ENOMEM, "host allocation failed");
+    }
+    for (int i = 0; i <= np; ++i) out->seg_offsets[i] = c->h_offsets[p0 + i] - s0;
+    if (out->n_seg > 0)
+        HIPCHK(hipMemcpyAsync(out->segments, c->csr.p + s0, sizeof(ccdgpu_segment) * out->n_seg, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(out->mask_bits, c->mask.p + (size_t)p0 * c->mask_words, sizeof(uint32_t) * (size_t)np * c->mask_words, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(out->procedure, c->procedure.p + p0, sizeof(int32_t) * np, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(out->probs, c->probs.p + 3 * p0, sizeof(double) * 3 * np, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(out->sorted_dates, c->sdates.p + (size_t)chip * no, sizeof(int64_t) * no, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(out->sort_index, c->order.p + (size_t)chip * no, sizeof(int32_t) * no, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < np; ++i)
+        if (out->procedure[i] < 0) {
+            out->error_pixel = i;
+            break;
+        }
+    return 0;
+}
+
+int ccdgpu_fetch_staged(ccdgpu_ctx *c, int32_t chip, ccdgpu_result *out) {
+    if (!c || !out) return fail(CCDGPU_EINVAL, "NULL argument");
+    return fetch_chip(c, chip, out);
+}
+
+int ccdgpu_detect_batch(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_pix, int32_t n_obs,
+                        const int64_t *dates, const int16_t *spectra, const uint16_t *qa, ccdgpu_result *out) {
+    if (!out) return fail(CCDGPU_EINVAL, "NULL result");
+    std::memset(out, 0, sizeof(*out));
+    auto t0 = std::chrono::steady_clock::now();
+    int rc = ccdgpu_stage(c, params, 1, n_pix, n_obs, dates, spectra, qa);
+    if (rc) return rc;
+    double ks = 0;
+    rc = ccdgpu_run_staged(c, &ks);
+    if (rc && rc != CCDGPU_EQA) return rc;
+    const int rc_qa = rc;
+    const std::string qa_msg = g_err;
+    rc = fetch_chip(c, 0, out);
+    if (rc) return rc;
+    out->seconds_kernel = ks;
+    out->seconds_total = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (rc_qa) g_err = qa_msg;
+    return rc_qa;
+}
+
+void ccdgpu_result_free(ccdgpu_result *r) {
+    if (!r) return;
+    std::free(r->seg_offsets);
+    std::free(r->segments);
+    std::free(r->mask_bits);
+    std::free(r->procedure);
+    std::free(r->probs);
+    std::free(r->sorted_dates);
+    std::free(r->sort_index);
+    std::memset(r, 0, sizeof(*r));
+}
+
+}  // extern "C"
