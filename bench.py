@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""bench.py -- pixels/s change-detected on MI355X (BASELINE.json metric), one JSON line.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--chips B] [--config C]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[2], the CONUS ARD tile the metric names):
+chips of a 5000x5000-pixel tile (2500 chips of 100x100 pixels, Landsat 4-8 1982-2017 cadence,
+synthetic ARD from libccdsynth).  Each rank (one process per GPU) owns B chips of the tile
+(chip ids rank*B .. rank*B+B-1 among the chips sharing the base cadence) staged in HBM; a
+"step" is one pass of the full detection hot path over those B chips: per-chip date sort +
+design rows, the per-pixel pyccd state machine, the per-pixel segment-count scan and the
+segment CSR scatter, results left in HBM.  Chips are independent: no data-path collective,
+weak scaling (fixed chips per GPU).  The timed region is bracketed by a barrier and a device
+synchronize on both sides; the reported time is the max over ranks.
+
+value = total pixels of all ranks / time.  roofline = counted FP64 flops of the detection
+kernel per launch / its HIP-event duration vs the MI355X FP64 peak (78.6 TFLOP/s; the path is
+FP64 vector ALU, not a GEMM).  cpu_baseline = the C restatement oracle (oracle/libccdoracle.so,
+"port") on a bounded sample of the same chips, on this host's cores.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, 'lcmap-firebird_amd'))
+
+import numpy as np  # noqa: E402
+
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (spec)
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E (spec)
+PIXELS_PER_CHIP = 10000
+TILE_CHIPS = 2500
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--chips', type=int, default=4, help='chips per GPU per step')
+    ap.add_argument('--config', type=int, default=3, help='synthetic config (2, 3, 4 or 5)')
+    ap.add_argument('--cpu-seconds', type=float, default=12.0, help='target CPU-baseline sample time')
+    ap.add_argument('--cpu-threads', type=int, default=16)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    return ap.parse_args()
+
+
+def chip_ids(cfg, rank, chips, synth):
+    """B chip ids of this rank that share the tile's base (non-sidelap) date vector, so the B
+    chips stage as one batch.  Rank r takes the r-th run of B such chips of the tile."""
+    base_n = synth.dates(cfg, 0).shape[0]
+    found = []
+    for c in range(TILE_CHIPS):
+        if synth.dates(cfg, c).shape[0] == base_n:
+            found.append(c)
+        if len(found) >= (rank + 1) * chips:
+            break
+    return found[rank * chips:(rank + 1) * chips]
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus and 'WORLD_SIZE' in os.environ:
+        print('warning: --gpus %d but WORLD_SIZE %d' % (args.gpus, world), file=sys.stderr)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+
+    import ccdgpu
+    from ccdgpu import synth
+
+    cfg = synth.config(args.config)
+    ids = chip_ids(cfg, rank, args.chips, synth)
+    dates = synth.dates(cfg, ids[0])
+    n_obs = dates.shape[0]
+    D = np.empty((len(ids), n_obs), np.int64)
+    S = np.empty((len(ids), 7, PIXELS_PER_CHIP, n_obs), np.int16)
+    Q = np.empty((len(ids), PIXELS_PER_CHIP, n_obs), np.uint16)
+    for j, c in enumerate(ids):
+        d, s, q = synth.chip(cfg, c, 0, PIXELS_PER_CHIP)
+        assert np.array_equal(d, dates)
+        D[j], S[j], Q[j] = d, s, q
+
+    ctx = ccdgpu.Context(local)
+    ctx.stage(D, S, Q)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        ctx.run()
+    barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    det_ms, prep_ms, flops, segs = [], [], 0, 0
+    for _ in range(args.steps):
+        ctx.run()
+        st = ctx.stats()
+        det_ms.append(st['detect_ms'])
+        prep_ms.append(st['prep_ms'])
+        flops = st['flops']
+        segs = st['segments']
+        alg_bytes = st['bytes']
+    ctx.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    pixels_total = world * len(ids) * PIXELS_PER_CHIP * args.steps
+    value = pixels_total / elapsed
+    det_avg = float(np.mean(det_ms))
+    achieved_tf = flops / (det_avg * 1e-3) / 1e12
+    traffic = None
+    pmc_path = os.path.join(ROOT, 'profiles', 'pmc_detect.json')
+    if os.path.exists(pmc_path):
+        try:
+            pmc = json.load(open(pmc_path))
+            if pmc.get('workload') == 'config%d_chips%d_nobs%d' % (args.config, args.chips, n_obs):
+                traffic = pmc.get('hbm_bytes_per_launch')
+        except Exception:
+            traffic = None
+
+    out = {
+        'metric': 'pixels/sec change-detected (CONUS ARD tile) at 1/2/4/8 MI355X; FP64 VALU %',
+        'value': value,
+        'unit': 'pixels/s',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': elapsed / args.steps * 1e3,
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'f64',
+        'data': 'synthetic (libccdsynth Landsat 4-8 ARD chips, seeded)',
+        'config': {
+            'workload': 'C3: CONUS ARD tile chips (100x100 px, L4-L8 1982-2017 cadence, %d obs/pixel), %d chips per GPU per step' % (n_obs, len(ids)),
+            'synthetic_config': args.config,
+            'chips_per_gpu': len(ids),
+            'pixels_per_chip': PIXELS_PER_CHIP,
+            'n_obs': n_obs,
+            'tile_chips': TILE_CHIPS,
+            'parallelism': 'chip-sharded x%d (one process per GPU, no collective)' % world,
+        },
+        'roofline': {
+            'bound': 'mfma',
+            'compute': 'fp64-valu',
+            'achieved': achieved_tf,
+            'peak': FP64_PEAK_TFLOPS,
+            'unit': 'TFLOP/s',
+            'frac': achieved_tf / FP64_PEAK_TFLOPS,
+            'traffic': traffic,
+            'kernel': 'ccd_detect',
+            'kernel_ms_per_launch': det_avg,
+            'flops_per_launch': flops,
+            'algorithmic_bytes_per_launch': alg_bytes,
+            'algorithmic_hbm_gbs': alg_bytes / (det_avg * 1e-3) / 1e9,
+            'hbm_peak_gbs': HBM_PEAK_GBS,
+        },
+        'segments_per_step': segs * world,
+        'prep_ms_per_launch': float(np.mean(prep_ms)),
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out['cpu_baseline'] = cpu_baseline(S[0], Q[0], dates, args)
+        out['speedup_vs_cpu_baseline'] = value / out['cpu_baseline']['value']
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(S, Q, dates, args):
+    """C restatement oracle (oracle/libccdoracle.so) on a bounded pixel sample of chip 0,
+    OpenMP over pixels on this host's cores."""
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    import oracle_ctypes
+    thr = args.cpu_threads
+    n_probe = 64 * thr
+    t = time.perf_counter()
+    oracle_ctypes.detect_batch(dates, S[:, :n_probe], Q[:n_probe], threads=thr)
+    rate = n_probe / (time.perf_counter() - t)
+    n = int(min(PIXELS_PER_CHIP, max(n_probe, rate * args.cpu_seconds)))
+    t = time.perf_counter()
+    oracle_ctypes.detect_batch(dates, S[:, :n], Q[:n], threads=thr)
+    el = time.perf_counter() - t
+    return {'value': n / el, 'unit': 'pixels/s', 'cores': thr, 'kind': 'port',
+            'sample': 'first %d pixels of chip 0 of the same workload (%.1f s), C restatement oracle, OpenMP' % (n, el)}
+
+
+if __name__ == '__main__':
+    main()

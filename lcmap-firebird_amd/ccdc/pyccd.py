@@ -1,0 +1,209 @@
+"""ccdc.pyccd -- the change-detection plugin boundary (mirror of reference ccdc/pyccd.py).
+
+Same names, signatures and row dicts as the reference (pyccd.py:27-183).  The only behavioural
+difference is the backend: ``ccd`` here is the MI355X shim (lcmap-firebird_amd/ccd), and ``rdd``
+batches each Spark partition's pixels by shared date vector (``mapPartitions``) instead of one
+``ccd.detect`` per pixel (``flatMap``, pyccd.py:183); the rows produced are identical.
+pyspark, cytoolz and merlin are optional here: the helpers they supplied are restated below.
+"""
+from datetime import date
+
+import numpy as np
+
+import ccd
+from ccdc import logger
+from ccdc._types import (ArrayType, ByteType, FloatType, IntegerType, StringType, StructField,
+                         StructType, require_pyspark)
+
+_NO_DEFAULT = object()
+
+
+# ---- cytoolz / merlin.functions helpers used by the reference module -------------------------
+def first(seq):
+    return next(iter(seq))
+
+
+def second(seq):
+    it = iter(seq)
+    next(it)
+    return next(it)
+
+
+def get(key, coll, default=_NO_DEFAULT):
+    """cytoolz.get: coll[key], or default when given and the key is missing."""
+    try:
+        return coll[key]
+    except (KeyError, IndexError, TypeError):
+        if default is _NO_DEFAULT:
+            raise
+        return default
+
+
+def get_in(keys, coll, default=None):
+    """cytoolz.get_in."""
+    try:
+        for k in keys:
+            coll = coll[k]
+        return coll
+    except (KeyError, IndexError, TypeError):
+        return default
+
+
+def denumpify(arg):
+    """merlin.functions.denumpify: numpy scalars/arrays -> native Python, containers kept."""
+    if isinstance(arg, np.generic):
+        return arg.item()
+    if isinstance(arg, np.ndarray):
+        return arg.tolist()
+    if isinstance(arg, dict):
+        return {k: denumpify(v) for k, v in arg.items()}
+    if isinstance(arg, list):
+        return [denumpify(v) for v in arg]
+    if isinstance(arg, tuple):
+        return tuple(denumpify(v) for v in arg)
+    return arg
+
+
+# ---- reference API ------------------------------------------------------------------------------
+def algorithm():
+    """Returns The ccd algorithm and version (pyccd.py:27-30)."""
+    return ccd.algorithm
+
+
+def table():
+    """Cassandra pyccd table name (pyccd.py:33-36)."""
+    return 'data'
+
+
+def schema():
+    """Spark schema of the ccd dataframe (pyccd.py:39-81)."""
+    return StructType([
+        StructField('cx', IntegerType(), nullable=False),
+        StructField('cy', IntegerType(), nullable=False),
+        StructField('px', IntegerType(), nullable=False),
+        StructField('py', IntegerType(), nullable=False),
+        StructField('sday', StringType(), nullable=False),
+        StructField('eday', StringType(), nullable=False),
+        StructField('bday', StringType(), nullable=True),
+        StructField('chprob', FloatType(), nullable=True),
+        StructField('curqa', IntegerType(), nullable=True),
+        StructField('blmag', FloatType(), nullable=True),
+        StructField('grmag', FloatType(), nullable=True),
+        StructField('remag', FloatType(), nullable=True),
+        StructField('nimag', FloatType(), nullable=True),
+        StructField('s1mag', FloatType(), nullable=True),
+        StructField('s2mag', FloatType(), nullable=True),
+        StructField('thmag', FloatType(), nullable=True),
+        StructField('blrmse', FloatType(), nullable=True),
+        StructField('grrmse', FloatType(), nullable=True),
+        StructField('rermse', FloatType(), nullable=True),
+        StructField('nirmse', FloatType(), nullable=True),
+        StructField('s1rmse', FloatType(), nullable=True),
+        StructField('s2rmse', FloatType(), nullable=True),
+        StructField('thrmse', FloatType(), nullable=True),
+        StructField('blcoef', ArrayType(FloatType()), nullable=True),
+        StructField('grcoef', ArrayType(FloatType()), nullable=True),
+        StructField('recoef', ArrayType(FloatType()), nullable=True),
+        StructField('nicoef', ArrayType(FloatType()), nullable=True),
+        StructField('s1coef', ArrayType(FloatType()), nullable=True),
+        StructField('s2coef', ArrayType(FloatType()), nullable=True),
+        StructField('thcoef', ArrayType(FloatType()), nullable=True),
+        StructField('blint', FloatType(), nullable=True),
+        StructField('grint', FloatType(), nullable=True),
+        StructField('reint', FloatType(), nullable=True),
+        StructField('niint', FloatType(), nullable=True),
+        StructField('s1int', FloatType(), nullable=True),
+        StructField('s2int', FloatType(), nullable=True),
+        StructField('thint', FloatType(), nullable=True),
+        StructField('dates', ArrayType(StringType()), nullable=False),
+        StructField('mask', ArrayType(ByteType()), nullable=True),
+        StructField('rfrawp', ArrayType(FloatType()), nullable=True),
+    ])
+
+
+def dataframe(ctx, rdd):
+    """Creates pyccd dataframe from an rdd of format() rows (pyccd.py:84-96)."""
+    require_pyspark('ccdc.pyccd.dataframe')
+    from pyspark.sql import SparkSession  # pragma: no cover
+    logger(ctx, name=__name__).debug('creating pyccd dataframe...')
+    return SparkSession(ctx).createDataFrame(rdd, schema())
+
+
+def default(change_models):
+    """No change models -> one day-1 placeholder row so the pixel is recorded (pyccd.py:99-103)."""
+    return [{'start_day': 1, 'end_day': 1, 'break_day': 1}] if not change_models else change_models
+
+
+def format(cx, cy, px, py, dates, ccdresult):
+    """One row dict per change model (pyccd.py:106-148).  ``dates`` in input order, ``mask`` in
+    pyccd's sorted-date order, exactly as the reference emits them."""
+    return [denumpify(
+        {'cx': cx,
+         'cy': cy,
+         'px': px,
+         'py': py,
+         'sday': date.fromordinal(get('start_day', cm)).isoformat(),
+         'eday': date.fromordinal(get('end_day', cm)).isoformat(),
+         'bday': date.fromordinal(get('break_day', cm, None)).isoformat(),
+         'chprob': get('change_probability', cm, None),
+         'curqa': get('curve_qa', cm, None),
+         'blmag': get_in(['blue', 'magnitude'], cm, None),
+         'grmag': get_in(['green', 'magnitude'], cm, None),
+         'remag': get_in(['red', 'magnitude'], cm, None),
+         'nimag': get_in(['nir', 'magnitude'], cm, None),
+         's1mag': get_in(['swir1', 'magnitude'], cm, None),
+         's2mag': get_in(['swir2', 'magnitude'], cm, None),
+         'thmag': get_in(['thermal', 'magnitude'], cm, None),
+         'blrmse': get_in(['blue', 'rmse'], cm, None),
+         'grrmse': get_in(['green', 'rmse'], cm, None),
+         'rermse': get_in(['red', 'rmse'], cm, None),
+         'nirmse': get_in(['nir', 'rmse'], cm, None),
+         's1rmse': get_in(['swir1', 'rmse'], cm, None),
+         's2rmse': get_in(['swir2', 'rmse'], cm, None),
+         'thrmse': get_in(['thermal', 'rmse'], cm, None),
+         'blcoef': get_in(['blue', 'coefficients'], cm, None),
+         'grcoef': get_in(['green', 'coefficients'], cm, None),
+         'recoef': get_in(['red', 'coefficients'], cm, None),
+         'nicoef': get_in(['nir', 'coefficients'], cm, None),
+         's1coef': get_in(['swir1', 'coefficients'], cm, None),
+         's2coef': get_in(['swir2', 'coefficients'], cm, None),
+         'thcoef': get_in(['thermal', 'coefficients'], cm, None),
+         'blint': get_in(['blue', 'intercept'], cm, None),
+         'grint': get_in(['green', 'intercept'], cm, None),
+         'reint': get_in(['red', 'intercept'], cm, None),
+         'niint': get_in(['nir', 'intercept'], cm, None),
+         's1int': get_in(['swir1', 'intercept'], cm, None),
+         's2int': get_in(['swir2', 'intercept'], cm, None),
+         'thint': get_in(['thermal', 'intercept'], cm, None),
+         'dates': [date.fromordinal(o).isoformat() for o in dates],
+         'mask': get('processing_mask', ccdresult, None)})
+        for cm in default(get('change_models', ccdresult, None))]
+
+
+def detect(timeseries):
+    """Takes in a timeseries ((cx, cy, px, py), {dates, blues..thermals, qas}) and returns a list
+    of detections (pyccd.py:151-168)."""
+    cx, cy, px, py = first(timeseries)
+    return format(cx=cx,
+                  cy=cy,
+                  px=px,
+                  py=py,
+                  dates=get('dates', second(timeseries)),
+                  ccdresult=ccd.detect(**second(timeseries)))
+
+
+def detect_partition(records, params=None):
+    """Batched detect over an iterable of timeseries records: pixels sharing a date vector go
+    to the GPU in one call; rows come out in record order, identical to ``detect``."""
+    records = list(records)
+    rows = []
+    for (key, res), (_, rec) in zip(ccd.detect_records(records, params), records):
+        cx, cy, px, py = key
+        rows.extend(format(cx=cx, cy=cy, px=px, py=py, dates=get('dates', rec), ccdresult=res))
+    return rows
+
+
+def rdd(ctx, timeseries):
+    """Run change detection against an RDD of timeseries (pyccd.py:171-183)."""
+    logger(context=ctx, name=__name__).info('executing change detection...')
+    return timeseries.mapPartitions(detect_partition)

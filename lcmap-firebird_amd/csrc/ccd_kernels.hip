@@ -69,6 +69,8 @@ struct Px {
     int64_t gpix;
     int nseg;
     unsigned long long fits, sweeps;
+    unsigned long long fl;       // counted FP64 flops, wave-uniform part
+    unsigned long long fl_lane;  // counted FP64 flops, per-lane part (coordinate descent)
 };
 
 // ------------------------------------------------------------------ wave primitives
@@ -357,8 +359,11 @@ __device__ void fit_models(Px &P, int a, int b, int k) {
         }
         L->coef[l][7] = L->ym[l] - dot;
         P.sweeps += (unsigned long long)sw;  // per-lane; reduced at the end
+        P.fl_lane += (unsigned long long)sw * (unsigned long long)(2 * pc * pc + 6 * pc) + 14;
     }
     P.fits += NB;
+    // means 14 n, centred Gram/X'y entries 4 n each, rmse 7 * (2*7 + 3) n
+    P.fl += (unsigned long long)nw * (unsigned long long)(14 + 4 * nE + 7 * 17) + 14;
     wsync();
     // rmse from residuals of the raw design (predict = X @ coef + intercept)
     double ss[NB] = {0, 0, 0, 0, 0, 0, 0};
@@ -476,6 +481,7 @@ __device__ void variogram(Px &P) {
         };
         const double med = median_int(gen, m - kk, cnt, 0, 65535);
         if (l == 0) L->vario[band] = med;
+        P.fl += (unsigned long long)(m - kk);
     }
     wsync();
 }
@@ -596,6 +602,8 @@ __device__ int tmask(Px &P, int a, int b) {
     const double w = 2.0 * M_PI / p.avg_days_yr;
     const double oc = w / ceil(((double)P.cd[b - 1] - (double)P.cd[a]) / p.avg_days_yr);
     const int ncol = (oc == w) ? 3 : 5;
+    // leverage + Gram (45 n) + per band: stats 4 n, OLS 60 n, <= 4 IRLS passes of 60 n + 18 n
+    P.fl += (unsigned long long)nw * (2 + 45 + 25);
     double *xoc = P.fs, *xos = P.fs + P.n, *adj = P.fs + 2 * P.n, *absr = P.fs + 3 * P.n,
            *wt = P.fs + 4 * P.n;
     // observation-cycle harmonics and flags
@@ -679,6 +687,7 @@ __device__ int tmask(Px &P, int a, int b) {
         const double ystd = sqrt(wsum(sv) / nw);
         double coef[5], coef0[5];
         tm_solve(P, a, nw, ncol, xoc, xos, band, nullptr, coef);
+        P.fl += (unsigned long long)nw * (4 + 60 + 12) + 120;
         int iteration = 1;
         bool converged = false;
         while (!converged && iteration < 5) {
@@ -716,6 +725,7 @@ __device__ int tmask(Px &P, int a, int b) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             wsync();
             tm_solve(P, a, nw, ncol, xoc, xos, band, wt, coef);
+            P.fl += (unsigned long long)nw * (60 + 18) + 120;
             iteration += 1;
             converged = true;
 #pragma unroll
@@ -770,6 +780,7 @@ __device__ bool stable(const Px &P, int a, int b) {
     }
     return sqrt(wsum(v2)) < P.chg;
 }
+__device__ __forceinline__ void count_stable(Px &P) { P.fl += 5 * (2 * 16 + 8) + 6; }
 
 __device__ bool initialize(Px &P, int &wa, int &wb) {
     const ccdgpu_params &p = P.A->p;
@@ -802,6 +813,7 @@ __device__ bool initialize(Px &P, int &wa, int &wb) {
             b -= cnt;
         }
         fit_models(P, a, b, 4);
+        count_stable(P);
         if (!stable(P, a, b)) { a += 1; b += 1; continue; }
         ok = true;
         break;
@@ -847,6 +859,7 @@ __device__ void lookback(Px &P, int &wa, int &wb, int prev) {
             for (int band = 0; band < NB; ++band) r[band] = resid_at(P, band, a - 1 - l);
             mag = magnitude(P, r, comp);
         }
+        P.fl += (unsigned long long)k * (7 * 16 + 5 * 4);
         const bool change = bal(l < k && !(mag > P.chg)) == 0ull;
         if (change) break;
         const double m0 = __shfl(mag, 0);
@@ -949,6 +962,8 @@ __device__ void lookforward(Px &P, int &wa, int &wb) {
             }
 #pragma unroll
             for (int band = 0; band < NB; ++band) comp[band] = sqrt(wsum(ss[band])) / 4.0;
+            // closest-DOY keys (5 flops) per selection pass, residuals of the 24 chosen obs
+            P.fl += (unsigned long long)nf * 5 * 13 + 24 * 7 * 18 + 7 * 2;
         }
         double mag = 0.0;
         if (l < k) {
@@ -956,6 +971,7 @@ __device__ void lookforward(Px &P, int &wa, int &wb) {
             for (int band = 0; band < NB; ++band) r[band] = resid_at(P, band, b + l);
             mag = magnitude(P, r, comp);
         }
+        P.fl += (unsigned long long)k * (7 * 16 + 5 * 4);
         const bool chg = bal(l < k && !(mag > P.chg)) == 0ull;
         if (chg) {
             change = 1.0;
@@ -1125,6 +1141,8 @@ __global__ __launch_bounds__(64) void ccd_detect(const CcdDetectArgs *__restrict
     P.fs = A.s_f64 + (size_t)slot * 5 * A.n_obs;
     P.fits = 0;
     P.sweeps = 0;
+    P.fl = 0;
+    P.fl_lane = 0;
     for (;;) {
         unsigned long long job = 0;
         if (l == 0) job = atomicAdd(&A.counters[0], 1ull);
@@ -1162,11 +1180,15 @@ __global__ __launch_bounds__(64) void ccd_detect(const CcdDetectArgs *__restrict
         wsync();
     }
     // instrumentation
-    unsigned long long sw = P.sweeps;
-    for (int o = 32; o > 0; o >>= 1) sw += __shfl_xor(sw, o);
+    unsigned long long sw = P.sweeps, fll = P.fl_lane;
+    for (int o = 32; o > 0; o >>= 1) {
+        sw += __shfl_xor(sw, o);
+        fll += __shfl_xor(fll, o);
+    }
     if (l == 0) {
         atomicAdd(&A.stats[0], P.fits);
         atomicAdd(&A.stats[1], sw);
+        atomicAdd(&A.stats[2], P.fl + fll);
     }
 }
 

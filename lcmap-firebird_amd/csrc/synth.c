@@ -75,7 +75,8 @@ static int cmp_i64(const void *a, const void *b) {
 }
 
 int ccdsynth_dates(const ccdsynth_cfg *cfg, int32_t chip, int64_t *out, int32_t cap) {
-    /* 16-day repeats: phase 0 = L4/L7, phase 8 = L5/L8; sidelap path +7 d on half the chips. */
+    /* 16-day repeats: phase 0 = L4/L7, phase 8 = L5/L8; sidelap path +7 d on half the chips (the
+     * sidelap acquisitions are per path, so every sidelap chip shares one date vector). */
     int64_t *buf = (int64_t *)malloc(sizeof(int64_t) * 8192);
     int n = 0;
     int side = cfg->sidelap && (mix64(cfg->seed ^ (uint64_t)chip * 77ull) & 1ull);
@@ -86,7 +87,7 @@ int ccdsynth_dates(const ccdsynth_cfg *cfg, int32_t chip, int64_t *out, int32_t 
         else on = (d >= ORD_L5_START && d <= ORD_L5_END) || d >= ORD_L8_START;
         if (!on) continue;
         buf[n++] = d;
-        if (side && d + 7 <= ORD_END && (hash5(cfg->seed, S_DATE, (uint64_t)chip, (uint64_t)d, 0) & 1ull))
+        if (side && d + 7 <= ORD_END && (hash5(cfg->seed, S_DATE, 0, (uint64_t)d, 0) & 1ull))
             buf[n++] = d + 7;
     }
     qsort(buf, (size_t)n, sizeof(int64_t), cmp_i64);

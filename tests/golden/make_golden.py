@@ -1,0 +1,131 @@
+"""Regenerate the golden vectors in tests/golden/ from oracle/ccd_ref.py (the numpy restatement
+of lcmap-pyccd ccd.detect).  Inputs come from the synthetic ARD generator (libccdsynth) plus
+hand-built edge cases; expected outputs are the restatement's change models and masks.
+
+    python tests/golden/make_golden.py            # ~1 min on 8 cores
+
+The reference itself (lcmap-pyccd) is not importable in this container, so these
+vectors pin the GPU path and the C oracle to the restatement; the restatement is pinned by the
+reference's own boundary tests (tests/test_reference_boundary.py)."""
+import json
+import multiprocessing
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [os.path.join(ROOT, 'lcmap-firebird_amd'), os.path.join(ROOT, 'oracle')]
+
+import numpy as np  # noqa: E402
+
+import ccd_ref  # noqa: E402
+from ccdgpu import abi, synth  # noqa: E402
+
+
+def run_pixel(args):
+    d, spec, q, params = args
+    r = ccd_ref.detect(d, *[spec[b] for b in range(7)], q, params=params)
+    return r
+
+
+def to_arrays(results, n_obs):
+    P = len(results)
+    words = (n_obs + 31) // 32
+    procedure = np.array([abi.PROCEDURES.index(r['procedure']) for r in results], dtype=np.int32)
+    mask = np.array([r['processing_mask'] for r in results], dtype=np.uint8).reshape(P, n_obs)
+    offsets = np.zeros(P + 1, dtype=np.int64)
+    segs = []
+    for i, r in enumerate(results):
+        for cm in r['change_models']:
+            s = np.zeros((), dtype=abi.SEGMENT_DTYPE)
+            for f in ('start_day', 'end_day', 'break_day', 'observation_count', 'curve_qa'):
+                s[f] = cm[f]
+            s['pixel'] = i
+            s['change_probability'] = cm['change_probability']
+            for b, name in enumerate(abi.BANDS):
+                s['magnitude'][b] = cm[name]['magnitude']
+                s['rmse'][b] = cm[name]['rmse']
+                s['intercept'][b] = cm[name]['intercept']
+                s['coef'][b] = cm[name]['coefficients']
+            segs.append(s)
+        offsets[i + 1] = len(segs)
+    segments = np.array(segs, dtype=abi.SEGMENT_DTYPE) if segs else np.zeros(0, dtype=abi.SEGMENT_DTYPE)
+    probs = np.array([[r['cloud_prob'], r['snow_prob'], r['water_prob']] for r in results], dtype=np.float64)
+    return dict(procedure=procedure, mask=np.packbits(mask, axis=1, bitorder='little'),
+                seg_offsets=offsets, segments=segments, probs=probs)
+
+
+def synth_case(which, chip, n_pix, **over):
+    cfg = synth.config(which, **over)
+    return synth.chip(cfg, chip, 0, n_pix)
+
+
+def edge_cases():
+    """Hand-built inputs exercising the branches the reference's tests and pyccd's procedures
+    name: the reference's all-fill element, few observations, insufficient clear, permanent
+    snow, duplicate dates, shuffled dates, L8 cirrus/occlusion QA, int16 thermal wrap."""
+    cases = {}
+    # reference test/__init__.py:37-46 timeseries_element (4 obs, qa = 1 fill)
+    d = np.array([734973, 731205, 724404, 723868], dtype=np.int64)
+    cases['ref_fill4'] = (d, np.full((7, 1, 4), -9999, dtype=np.int16), np.ones((1, 4), dtype=np.uint16))
+    base_d, base_s, base_q = synth_case(2, 5, 8)
+    n = base_d.shape[0]
+    order = np.argsort(base_d)
+    # few observations: only the last 20 dates clear -> END catch only
+    s1, q1 = np.full((7, 1, n), -9999, dtype=np.int16), np.ones((1, n), dtype=np.uint16)
+    q1[0, order[-20:]] = 66
+    s1[:, 0, order[-20:]] = base_s[:, 1, order[-20:]].clip(100, 5000)
+    s1[6, 0, order[-20:]] = 2950
+    # insufficient clear: 15 % clear, rest cloud
+    rng = np.random.default_rng(7)
+    s2, q2 = base_s[:, 2:3].copy(), np.full((1, n), 224, dtype=np.uint16)
+    pick = rng.choice(n, size=int(0.15 * n), replace=False)
+    q2[0, pick] = 66
+    s2[:, 0, pick] = np.array([500, 800, 700, 2800, 2000, 1200, 2900], dtype=np.int16)[:, None] + rng.integers(-40, 40, size=(7, pick.size)).astype(np.int16)
+    # permanent snow: 10 % clear, 70 % snow
+    s3, q3 = s2.copy(), np.full((1, n), 224, dtype=np.uint16)
+    q3[0, pick[:len(pick) * 2 // 3]] = 66
+    snow = rng.choice(np.setdiff1d(np.arange(n), pick), size=int(0.7 * n), replace=False)
+    q3[0, snow] = 80
+    s3[:, 0, snow] = np.array([6000, 6200, 6300, 5500, 400, 300, 2600], dtype=np.int16)[:, None]
+    spectra = np.concatenate([s1, s2, s3, base_s[:, 3:6]], axis=1)
+    qa = np.concatenate([q1, q2, q3, base_q[3:6]], axis=0)
+    # pixel 5: L8 cirrus (768 = bits 8,9) / occlusion (1024) values on its clear obs
+    qa[4, order[-60::3]] = 768
+    qa[4, order[-59::3]] = 1024
+    # pixel 5: hot thermal (K*10 > 3276.7 wraps in int16 after *10-27315)
+    spectra[6, 5, order[200:260:5]] = 3400
+    cases['mixed_edge'] = (base_d, spectra, qa)
+    # duplicate dates: every 10th date duplicated (copy with different values), shuffled input order
+    dd = np.concatenate([base_d, base_d[::10]])
+    ss = np.concatenate([base_s[:, :4], base_s[:, 4:8, ::10]], axis=2)
+    qq = np.concatenate([base_q[:4], base_q[4:8, ::10]], axis=1)
+    perm = np.random.default_rng(11).permutation(dd.shape[0])
+    cases['dup_shuffled'] = (dd[perm], ss[:, :, perm], qq[:, perm])
+    return cases
+
+
+def main():
+    cases = {
+        'c2_chip11': (synth_case(2, 11, 16), None),
+        'c4_chip11': (synth_case(4, 11, 16), None),
+        'c5_chip3_sidelap': (synth_case(5, 3, 10), None),
+        'c3_chip4_sidelap': (synth_case(3, 4, 6), None),
+        'c5_chip11_fixedpeek': (synth_case(5, 11, 8), {'ADAPTIVE_PEEK': False}),
+        'c2_chip11_rmsedof': (synth_case(2, 11, 6), {'RMSE_DOF': True}),
+    }
+    for name, inp in edge_cases().items():
+        cases[name] = (inp, None)
+    with multiprocessing.Pool(min(8, os.cpu_count() or 1)) as pool:
+        for name, ((d, s, q), params) in cases.items():
+            jobs = [(d, s[:, p], q[p], params) for p in range(q.shape[0])]
+            results = pool.map(run_pixel, jobs)
+            out = to_arrays(results, d.shape[0])
+            np.savez_compressed(os.path.join(HERE, name + '.npz'), dates=d, spectra=s, qa=q,
+                                params=np.array(json.dumps(params or {})), **out)
+            print(name, 'pixels', q.shape[0], 'obs', d.shape[0], 'segments', len(out['segments']),
+                  'procedures', np.bincount(out['procedure'], minlength=3).tolist(), flush=True)
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,58 @@
+"""C-ABI checks that need no GPU: the libraries load, export every symbol the headers declare,
+and the struct layouts agree between include/ccdgpu.h and the ctypes mirror."""
+import ctypes
+import os
+import re
+
+import pytest
+
+import ccdgpu
+from ccdgpu import abi, synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared(header):
+    txt = open(os.path.join(ROOT, 'include', header)).read()
+    return sorted(set(re.findall(r'\b(ccd(?:gpu|synth)_[a-z_]+)\s*\(', txt)))
+
+
+def test_libccdgpu_exports_every_declared_symbol():
+    L = ccdgpu.lib()
+    names = declared('ccdgpu.h')
+    assert 'ccdgpu_detect_batch' in names
+    for n in names:
+        assert hasattr(L, n), n
+    assert set(names) == set(ccdgpu.EXPORTS)
+
+
+def test_libccdsynth_exports_every_declared_symbol():
+    L = synth.lib()
+    for n in declared('ccdsynth.h'):
+        assert hasattr(L, n), n
+
+
+def test_struct_sizes_and_defaults():
+    assert ctypes.sizeof(abi.Segment) == 4 * 6 + 8 + 8 * (7 * 3 + 49)
+    p = ccdgpu.default_params()  # host-only entry point, no device needed
+    q = abi.default_params()
+    for name, _ in abi.Params._fields_:
+        assert getattr(p, name) == getattr(q, name), name
+    assert 'gfx950' in ccdgpu.version()
+
+
+def test_params_from_pyccd_dict():
+    p = abi.params_from_dict({'PEEK_SIZE': 8, 'DETECTION_BANDS': [1, 3], 'CURVE_QA': {'START': 15},
+                              'ADAPTIVE_PEEK': False})
+    assert p.peek_size == 8 and p.detection_bands == 0b1010 and p.curve_qa_start == 15
+    assert p.adaptive_peek == 0
+    with pytest.raises(KeyError):
+        abi.params_from_dict({'NOT_A_PARAM': 1})
+
+
+def test_init_without_gpu_fails_loudly():
+    """No CPU fallback: on a host with no gfx950 device the context refuses to come up."""
+    if ccdgpu.device_count() > 0:
+        pytest.skip('a GPU is visible')
+    with pytest.raises(ccdgpu.CcdGpuError):
+        ccdgpu.Context(0)

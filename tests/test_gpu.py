@@ -1,0 +1,161 @@
+"""GPU parity tests: the HIP path (through the C-ABI) against the golden vectors and the C
+oracle, at golden, chip and maximum sizes, plus size-independent properties.  Integer outputs
+(procedure, mask, segment count, days, observation counts, curve QA) must be bit-exact; floats
+within 1e-6 relative (tests/parity_util.py)."""
+import numpy as np
+import pytest
+
+import ccdgpu
+import golden_util
+import oracle_ctypes
+import parity_util
+from ccdgpu import abi, synth
+
+pytestmark = pytest.mark.gpu
+
+ORACLE_THREADS = 16
+
+
+@pytest.fixture(scope='module')
+def ctx():
+    c = ccdgpu.Context(0)
+    yield c
+    c.close()
+
+
+def assert_parity(got, ref):
+    problems, max_rel = parity_util.compare(got, ref)
+    assert not problems, problems[:10]
+    assert max_rel < parity_util.RTOL
+
+
+@pytest.mark.parametrize('name', golden_util.names())
+def test_golden(ctx, name):
+    (d, s, q), params, ref = golden_util.load(name)
+    got = ctx.detect_batch(d, s, q, params=params)
+    assert_parity(got, ref)
+
+
+@pytest.mark.parametrize('which,chip,n_pix', [(2, 0, 10000), (4, 1, 10000), (5, 3, 4000), (3, 5, 2000)])
+def test_chip_vs_oracle(ctx, which, chip, n_pix):
+    d, s, q = synth.chip(synth.config(which), chip, 0, n_pix)
+    got = ctx.detect_batch(d, s, q)
+    rc, ref = oracle_ctypes.detect_batch(d, s, q, threads=ORACLE_THREADS)
+    assert rc == 0
+    assert_parity(got, ref)
+    assert got.segments.shape[0] >= n_pix * (10 if which == 5 else 1) * 0.9
+
+
+@pytest.mark.parametrize('params', [
+    {'ADAPTIVE_PEEK': False},
+    {'RMSE_DOF': True},
+    {'PEEK_SIZE': 8, 'ADAPTIVE_PEEK': False},
+    {'T_CONST': 4.89, 'CHANGE_PROBABILITY': 0.95},
+    {'DETECTION_BANDS': [1, 3, 4], 'TMASK_BANDS': [2, 4]},
+    {'KELVIN_TO_CELSIUS': False, 'THERMAL_MIN': 1800, 'THERMAL_MAX': 3400},
+    {'COEFFICIENT_MAX': 6, 'LASSO_MAX_ITER': 50},
+])
+def test_param_variants_vs_oracle(ctx, params):
+    d, s, q = synth.chip(synth.config(5), 4, 0, 300)
+    got = ctx.detect_batch(d, s, q, params=params)
+    rc, ref = oracle_ctypes.detect_batch(d, s, q, params=params, threads=ORACLE_THREADS)
+    assert rc == 0
+    assert_parity(got, ref)
+
+
+def test_max_observations(ctx):
+    """CCDGPU_MAX_OBS dates per pixel (every ~3 days over 1982-2017)."""
+    n = abi.MAX_OBS
+    d = np.linspace(723868, 736694, n).round().astype(np.int64)
+    d = np.unique(d)
+    d = np.concatenate([d, d[: n - d.shape[0]] + 1])[:n]
+    cfg = synth.config(2)
+    _, s, q = synth.chip(cfg, 3, 0, 48, chip_dates=d)
+    got = ctx.detect_batch(d, s, q)
+    rc, ref = oracle_ctypes.detect_batch(d, s, q, threads=ORACLE_THREADS)
+    assert rc == 0
+    assert_parity(got, ref)
+    with pytest.raises(ccdgpu.CcdGpuError):
+        dd = np.arange(n + 1, dtype=np.int64) + 723868
+        ctx.detect_batch(dd, np.zeros((7, 1, n + 1), np.int16), np.ones((1, n + 1), np.uint16))
+
+
+def test_input_order_invariance(ctx):
+    """Size-independent property: results do not depend on the order merlin delivers dates in."""
+    d, s, q = synth.chip(synth.config(5), 2, 0, 2000)
+    a = ctx.detect_batch(d, s, q)
+    perm = np.random.default_rng(5).permutation(d.shape[0])
+    b = ctx.detect_batch(d[perm], s[:, :, perm], q[:, perm])
+    assert np.array_equal(a.mask, b.mask)
+    assert np.array_equal(a.seg_offsets, b.seg_offsets)
+    assert a.segments.tobytes() == b.segments.tobytes()
+
+
+def test_pixel_batch_independence(ctx):
+    """A pixel's result does not depend on which other pixels share its launch."""
+    d, s, q = synth.chip(synth.config(2), 6, 0, 512)
+    full = ctx.detect_batch(d, s, q)
+    for px in (0, 17, 511):
+        one = ctx.detect_batch(d, s[:, px:px + 1], q[px:px + 1])
+        a, b = full.seg_offsets[px], full.seg_offsets[px + 1]
+        assert one.segments.shape[0] == b - a
+        x = full.segments[a:b].copy()
+        x['pixel'] = 0
+        assert x.tobytes() == one.segments.tobytes()
+        assert np.array_equal(one.mask[0], full.mask[px])
+
+
+def test_staged_multichip_matches_single(ctx):
+    cfg = synth.config(2)
+    chips = [synth.chip(cfg, c, 0, 700) for c in (0, 1, 2)]
+    d = np.stack([c[0] for c in chips])
+    s = np.stack([c[1] for c in chips])
+    q = np.stack([c[2] for c in chips])
+    ctx.stage(d, s, q)
+    ctx.run()
+    st = ctx.stats()
+    assert st['pixels'] == 2100 and st['segments'] > 0
+    for i in range(3):
+        got = ctx.fetch(i)
+        ref = ctx.detect_batch(*chips[i])
+        assert got.segments.tobytes() == ref.segments.tobytes()
+        assert np.array_equal(got.mask, ref.mask)
+
+
+def test_unsupported_qa_raises_value_error(ctx):
+    d, s, q = synth.chip(synth.config(2), 1, 0, 4)
+    q = q.copy()
+    q[2, 10] = 64
+    with pytest.raises(ValueError) as ei:
+        ctx.detect_batch(d, s, q)
+    assert ei.value.result.error_pixel == 2
+
+
+def test_ccd_detect_api_and_reference_known_answer():
+    """ccd.detect (pyccd signature) and pyccd.detect(timeseries_element) on the GPU:
+    reference test_pyccd.py:129-132."""
+    import ccd
+    from ccdc import pyccd
+    from test_reference_boundary import CCD_FORMAT_KEYS, TIMESERIES_ELEMENT
+    rows = pyccd.detect(TIMESERIES_ELEMENT)
+    assert len(rows) == 1 and rows[0]['cx'] == -1815585
+    assert set(rows[0].keys()) == set(CCD_FORMAT_KEYS)
+    assert rows[0]['mask'] == [0, 0, 0, 0] and rows[0]['bday'] == '0001-01-01'
+    (d, s, q), params, ref = golden_util.load('c5_chip3_sidelap')
+    for px in (0, 3):
+        r = ccd.detect(d, *[s[b, px] for b in range(7)], q[px], params=params or None)
+        a, b = ref.seg_offsets[px], ref.seg_offsets[px + 1]
+        assert [cm['break_day'] for cm in r['change_models']] == list(ref.segments['break_day'][a:b])
+        assert np.array_equal(np.array(r['processing_mask'], bool), ref.mask[px])
+        assert 'lcmap-pyccd' in r['algorithm']
+    empty = ccd.detect([], [], [], [], [], [], [], [], [])
+    assert empty['change_models'] == [] and empty['processing_mask'] == []
+    with pytest.raises(AssertionError):
+        ccd.detect([1, 2], [1], [1], [1], [1], [1], [1], [1], [1, 2])
+
+
+def test_native_library_is_what_ran(ctx):
+    d, s, q = synth.chip(synth.config(2), 0, 0, 2)
+    ctx.detect_batch(d, s, q)
+    maps = open('/proc/self/maps').read()
+    assert 'libccdgpu.so' in maps

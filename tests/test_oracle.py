@@ -1,0 +1,82 @@
+"""CPU tests of the oracles themselves (no GPU): the C restatement (oracle/libccdoracle.so)
+against the golden vectors minted by the numpy restatement, and the numpy restatement's Lasso
+sub-kernel against the installed scikit-learn."""
+import warnings
+
+import numpy as np
+import pytest
+
+import ccd_ref
+import golden_util
+import oracle_ctypes
+import parity_util
+from ccdgpu import abi, synth
+
+
+@pytest.mark.parametrize('name', golden_util.names())
+def test_c_oracle_matches_golden(name):
+    (d, s, q), params, ref = golden_util.load(name)
+    rc, got = oracle_ctypes.detect_batch(d, s, q, params=params, threads=4)
+    assert rc == 0
+    problems, max_rel = parity_util.compare(got, ref)
+    assert not problems, problems
+    assert max_rel < 1e-6
+
+
+def test_numpy_restatement_reproduces_golden_edges():
+    for name in ('ref_fill4', 'mixed_edge'):
+        (d, s, q), params, ref = golden_util.load(name)
+        for px in range(q.shape[0]):
+            r = ccd_ref.detect(d, *[s[b, px] for b in range(7)], q[px], params=params)
+            assert abi.PROCEDURES.index(r['procedure']) == ref.procedure[px]
+            assert np.array_equal(np.array(r['processing_mask'], dtype=bool), ref.mask[px])
+            a, b = ref.seg_offsets[px], ref.seg_offsets[px + 1]
+            assert len(r['change_models']) == b - a
+
+
+def test_lasso_port_matches_installed_sklearn():
+    """models/lasso.fitted_model = sklearn Lasso(max_iter=1000).fit on coefficient_matrix:
+    the restatement's port of sklearn 0.18's coordinate descent agrees with sklearn 1.7.2."""
+    from sklearn.linear_model import Lasso
+    P = ccd_ref.get_params()
+    d, s, q = synth.chip(synth.config(2), 2, 0, 4)
+    o = np.argsort(d)
+    d = d[o]
+    rng = np.random.default_rng(0)
+    worst = 0.0
+    for trial in range(60):
+        n = int(rng.integers(12, 300))
+        st = int(rng.integers(0, len(d) - n))
+        k = (4, 6, 8)[trial % 3]
+        dd = d[st:st + n]
+        y = s[int(rng.integers(0, 7)), int(rng.integers(0, 4))][o][st:st + n].astype(float)
+        f = ccd_ref.fitted_model(dd, y, P, k)
+        X = ccd_ref.coefficient_matrix(dd, P.AVG_DAYS_YR, k)
+        with warnings.catch_warnings():
+            warnings.simplefilter('ignore')
+            m = Lasso(max_iter=1000).fit(X, y)
+        nz = np.abs(m.coef_) > 0
+        rel = np.max(np.abs(m.coef_ - f.coef)[nz] / np.abs(m.coef_)[nz]) if nz.any() else 0.0
+        worst = max(worst, rel, abs(m.intercept_ - f.intercept) / abs(m.intercept_))
+    assert worst < 1e-6, worst
+
+
+def test_chi2_thresholds():
+    """CHANGE/OUTLIER thresholds are chi2.ppf(0.99 / 0.999999, 5); the C oracle's inverse cdf
+    (used for the ncompare adjusted threshold) agrees with scipy."""
+    from scipy.stats import chi2
+    P = ccd_ref.get_params()
+    assert P.CHANGE_THRESHOLD == pytest.approx(chi2.ppf(0.99, 5), rel=1e-15)
+    assert P.OUTLIER_THRESHOLD == pytest.approx(chi2.ppf(0.999999, 5), rel=1e-15)
+    L = oracle_ctypes.lib()
+    for peek in (7, 8, 12, 20, 64):
+        pt = 1 - (1 - 0.99) ** (6 / peek)
+        assert L.ccdoracle_chi2_5_ppf(pt) == pytest.approx(chi2.ppf(pt, 5), rel=1e-12)
+
+
+def test_oracle_unsupported_qa_is_an_error():
+    d, s, q = synth.chip(synth.config(2), 1, 0, 3)
+    q = q.copy()
+    q[1, 17] = 64  # only bit 6 set: pyccd qa.qabitval raises ValueError
+    rc, u = oracle_ctypes.detect_batch(d, s, q, threads=2)
+    assert rc == abi.E_QA and u.error_pixel == 1

@@ -14,7 +14,7 @@ for which in (2, 4, 5):
     cfg = synth.config(which)
     d, s, q = synth.chip(cfg, 11, 0, npix)
     t = time.time(); u = ctx.detect_batch(d, s, q); tg = time.time() - t
-    t = time.time(); rc, r = oracle_ctypes.detect_batch(d, s, q); to = time.time() - t
+    t = time.time(); rc, r = oracle_ctypes.detect_batch(d, s, q, threads=16); to = time.time() - t
     probs, mr = parity_util.compare(u, r)
     print('config %d npix %d: gpu %.3fs (kernel %.3fs) oracle %.3fs segs %d/%d problems %d maxrel %.2e' % (
         which, npix, tg, u.seconds_kernel, to, len(u.segments), len(r.segments), len(probs), mr), flush=True)
