@@ -33,7 +33,8 @@ struct CcdDetectArgs {
     const int32_t *order;
     const int64_t *sdates;
     const double *basis;
-    // work queue + global flags: [0] next pixel, [1] pool count, [2] error pixel+1 (min), [3] overflow
+    // work queue + global flags: [0] next pixel, [1] pool count, [2] first QA-error pixel (min),
+    // [3] pool overflow, [4] first source line whose index guard tripped (0 = none)
     unsigned long long *counters;
     // per-slot scratch
     int32_t *s_date;

@@ -73,6 +73,30 @@ struct Px {
     unsigned long long fl_lane;  // counted FP64 flops, per-lane part (coordinate descent)
 };
 
+// ------------------------------------------------------------------ index guards
+// Every read of the compacted period goes through these: an out-of-range index is clamped (so a
+// logic error can never fault the GPU) and the first offending source line is recorded in
+// counters[4]; the host turns a nonzero value into CCDGPU_EHIP with that line number.
+__device__ __noinline__ void ccd_flag(const Px &P, int line) {
+    atomicCAS(&P.A->counters[4], 0ull, (unsigned long long)line);
+}
+__device__ __forceinline__ int gidx(const Px &P, int j, int lim, int line) {
+    if ((unsigned)j < (unsigned)lim) return j;
+    ccd_flag(P, line);
+    return 0;
+}
+__device__ __forceinline__ int32_t cdr(const Px &P, int j, int line) { return P.cd[gidx(P, j, P.m, line)]; }
+__device__ __forceinline__ int cir(const Px &P, int j, int line) {
+    const int c = P.ci[gidx(P, j, P.m, line)];
+    return gidx(P, c, P.n, line);
+}
+__device__ __forceinline__ int16_t cvr(const Px &P, int b, int j, int line) {
+    return P.cv[(size_t)b * P.n + gidx(P, j, P.m, line)];
+}
+#define CDR(P, j) cdr(P, (j), __LINE__)
+#define CIR(P, j) cir(P, (j), __LINE__)
+#define CVR(P, b, j) cvr(P, (b), (j), __LINE__)
+
 // ------------------------------------------------------------------ wave primitives
 __device__ __forceinline__ int lane() { return (int)__lane_id(); }
 __device__ __forceinline__ unsigned long long bal(bool p) { return __ballot(p); }
@@ -87,7 +111,7 @@ __device__ __forceinline__ double wsum(double v) {
 }
 __device__ __forceinline__ void wsync() { __syncthreads(); }
 
-__device__ __forceinline__ double cvalf(const Px &P, int b, int j) { return (double)P.cv[(size_t)b * P.n + j]; }
+#define cvalf(P, b, j) ((double)CVR(P, b, j))
 
 // k-th smallest (0-based) of integer values in [lo, hi] produced by gen(i, &v) (returns valid).
 template <class F>
@@ -175,7 +199,7 @@ __device__ int compact_drop(Px &P, int a, F drop) {
         const unsigned long long keep = bal(in && !dr);
         if (in && dr) atomicAnd(&P.L->mask[c >> 5], ~(1u << (c & 31)));
         if (in && !dr) {
-            const int pos = out + below(keep);
+            const int pos = gidx(P, out + below(keep), P.n, __LINE__);
             P.cd[pos] = d;
             P.ci[pos] = c;
 #pragma unroll
@@ -194,9 +218,9 @@ __device__ __forceinline__ void stage_rows(const Px &P, int j0, int cnt) {
     const int l = lane();
     if (l < cnt) {
         const int j = j0 + l;
-        const double *bs = P.basis + (size_t)P.ci[j] * CCD_BASIS_STRIDE;
+        const double *bs = P.basis + (size_t)CIR(P, j) * CCD_BASIS_STRIDE;
         double *r = P.L->row[l];
-        r[0] = (double)P.cd[j];
+        r[0] = (double)CDR(P, j);
 #pragma unroll
         for (int c = 1; c < 7; ++c) r[c] = bs[c];
 #pragma unroll
@@ -370,8 +394,8 @@ __device__ void fit_models(Px &P, int a, int b, int k) {
     for (int t0 = 0; t0 < nw; t0 += W) {
         const int j = a + t0 + l;
         if (t0 + l < nw) {
-            const double *bs = P.basis + (size_t)P.ci[j] * CCD_BASIS_STRIDE;
-            const double x0 = (double)P.cd[j];
+            const double *bs = P.basis + (size_t)CIR(P, j) * CCD_BASIS_STRIDE;
+            const double x0 = (double)CDR(P, j);
 #pragma unroll
             for (int band = 0; band < NB; ++band) {
                 const double *c = L->coef[band];
@@ -395,9 +419,9 @@ __device__ void fit_models(Px &P, int a, int b, int k) {
 
 // residual of band b at compacted observation j for the current models (lasso.predict)
 __device__ __forceinline__ double resid_at(const Px &P, int band, int j) {
-    const double *bs = P.basis + (size_t)P.ci[j] * CCD_BASIS_STRIDE;
+    const double *bs = P.basis + (size_t)CIR(P, j) * CCD_BASIS_STRIDE;
     const double *c = P.L->coef[band];
-    double pr = (double)P.cd[j] * c[0];
+    double pr = (double)CDR(P, j) * c[0];
 #pragma unroll
     for (int jj = 1; jj < 7; ++jj) pr += bs[jj] * c[jj];
     pr += c[7];
@@ -440,8 +464,8 @@ __device__ void emit(Px &P, int sday, int eday, int bday, int count, double chpr
 
 __device__ void catch_(Px &P, int a, int b, int cqa) {
     fit_models(P, a, b, P.A->p.coef_min);
-    const int bday = b < P.m ? P.cd[b] : P.cd[P.m - 1];
-    emit(P, P.cd[a], P.cd[b - 1], bday, b - a, 0.0, cqa, 0.0);
+    const int bday = b < P.m ? CDR(P, b) : CDR(P, P.m - 1);
+    emit(P, CDR(P, a), CDR(P, b - 1), bday, b - a, 0.0, cqa, 0.0);
 }
 
 // ------------------------------------------------------------------ variogram / peek
@@ -459,7 +483,7 @@ __device__ void variogram(Px &P) {
         int cnt = 0;
         for (int base = 0; base < m - k; base += W) {
             const int i = base + l;
-            cnt += popc(bal(i < m - k && (P.cd[i + k] - P.cd[i]) > 30));
+            cnt += popc(bal(i < m - k && (CDR(P, i + k) - CDR(P, i)) > 30));
         }
         if (2 * cnt >= m - k) { lag = k; break; }
     }
@@ -468,13 +492,13 @@ __device__ void variogram(Px &P) {
     int cnt = 0;
     for (int base = 0; base < m - kk; base += W) {
         const int i = base + l;
-        cnt += popc(bal(i < m - kk && (all || (P.cd[i + kk] - P.cd[i]) > 30)));
+        cnt += popc(bal(i < m - kk && (all || (CDR(P, i + kk) - CDR(P, i)) > 30)));
     }
     for (int band = 0; band < NB; ++band) {
         const int16_t *v = P.cv + (size_t)band * P.n;
         auto gen = [&](int i, int &val) -> bool {
             if (i >= m - kk) return false;
-            if (!all && (P.cd[i + kk] - P.cd[i]) <= 30) return false;
+            if (!all && (CDR(P, i + kk) - CDR(P, i)) <= 30) return false;
             int d = (int)v[i + kk] - (int)v[i];
             val = d < 0 ? -d : d;
             return true;
@@ -492,7 +516,7 @@ __device__ void adjust_peek(Px &P) {
     P.chg = p.change_threshold;
     if (!p.adaptive_peek || P.m < 2) return;
     auto gen = [&](int i, int &val) -> bool {
-        val = P.cd[i + 1] - P.cd[i];
+        val = CDR(P, i + 1) - CDR(P, i);
         return true;
     };
     const double delta = median_int(gen, P.m - 1, P.m - 1, 0, 1 << 20);
@@ -545,7 +569,7 @@ __device__ bool tm_solve(const Px &P, int a, int nw, int ncol, const double *xoc
     for (int t0 = 0; t0 < nw; t0 += W) {
         const int i = t0 + l;
         if (i < nw) {
-            const double *bs = P.basis + (size_t)P.ci[a + i] * CCD_BASIS_STRIDE;
+            const double *bs = P.basis + (size_t)CIR(P, a + i) * CCD_BASIS_STRIDE;
             double x[5];
             x[0] = bs[1];
             x[1] = bs[2];
@@ -586,7 +610,7 @@ __device__ bool tm_solve(const Px &P, int a, int nw, int ncol, const double *xoc
 }
 
 __device__ __forceinline__ double tm_pred(const Px &P, int j, int ncol, double xc, double xs, const double *coef) {
-    const double *bs = P.basis + (size_t)P.ci[j] * CCD_BASIS_STRIDE;
+    const double *bs = P.basis + (size_t)CIR(P, j) * CCD_BASIS_STRIDE;
     double pr = bs[1] * coef[0] + bs[2] * coef[1];
     if (ncol == 5) pr += xc * coef[2] + xs * coef[3] + coef[4];
     else pr += coef[2];
@@ -600,7 +624,7 @@ __device__ int tmask(Px &P, int a, int b) {
     const int l = lane();
     const int nw = b - a;
     const double w = 2.0 * M_PI / p.avg_days_yr;
-    const double oc = w / ceil(((double)P.cd[b - 1] - (double)P.cd[a]) / p.avg_days_yr);
+    const double oc = w / ceil(((double)CDR(P, b - 1) - (double)CDR(P, a)) / p.avg_days_yr);
     const int ncol = (oc == w) ? 3 : 5;
     // leverage + Gram (45 n) + per band: stats 4 n, OLS 60 n, <= 4 IRLS passes of 60 n + 18 n
     P.fl += (unsigned long long)nw * (2 + 45 + 25);
@@ -610,7 +634,7 @@ __device__ int tmask(Px &P, int a, int b) {
     for (int t0 = 0; t0 < nw; t0 += W) {
         const int i = t0 + l;
         if (i < nw && ncol == 5) {
-            const double t = (double)P.cd[a + i];
+            const double t = (double)CDR(P, a + i);
             double sv, cv;
             sincos(oc * t, &sv, &cv);
             xoc[i] = cv;
@@ -629,7 +653,7 @@ __device__ int tmask(Px &P, int a, int b) {
         for (int t0 = 0; t0 < nw; t0 += W) {
             const int i = t0 + l;
             if (i < nw) {
-                const double *bs = P.basis + (size_t)P.ci[a + i] * CCD_BASIS_STRIDE;
+                const double *bs = P.basis + (size_t)CIR(P, a + i) * CCD_BASIS_STRIDE;
                 double x[5] = {bs[1], bs[2], ncol == 5 ? xoc[i] : 1.0, ncol == 5 ? xos[i] : 0.0,
                                ncol == 5 ? 1.0 : 0.0};
                 int e = 0;
@@ -652,7 +676,7 @@ __device__ int tmask(Px &P, int a, int b) {
         for (int t0 = 0; t0 < nw; t0 += W) {
             const int i = t0 + l;
             if (i < nw) {
-                const double *bs = P.basis + (size_t)P.ci[a + i] * CCD_BASIS_STRIDE;
+                const double *bs = P.basis + (size_t)CIR(P, a + i) * CCD_BASIS_STRIDE;
                 double x[5] = {bs[1], bs[2], ncol == 5 ? xoc[i] : 1.0, ncol == 5 ? xos[i] : 0.0, 1.0};
                 double h = 0.9999;
                 if (ok) {
@@ -774,7 +798,7 @@ __device__ bool stable(const Px &P, int a, int b) {
         const double rm = L->rmse[l];
         const double vr = L->vario[l];
         const double rn = rm > vr ? rm : vr;
-        const double slope = L->coef[l][0] * ((double)P.cd[b - 1] - (double)P.cd[a]);
+        const double slope = L->coef[l][0] * ((double)CDR(P, b - 1) - (double)CDR(P, a));
         const double v = (fabs(slope) + fabs(resid_at(P, l, a)) + fabs(resid_at(P, l, b - 1))) / rn;
         v2 = v * v;
     }
@@ -789,7 +813,7 @@ __device__ bool initialize(Px &P, int &wa, int &wb) {
     int a = wa, b = wb;
     bool ok = false;
     while (b + p.meow_size < P.m) {
-        if (P.cd[b - 1] - P.cd[a] < p.day_delta) { b += 1; continue; }
+        if (CDR(P, b - 1) - CDR(P, a) < p.day_delta) { b += 1; continue; }
         const int cnt = tmask(P, a, b);
         const int nw = b - a;
         if (cnt == nw) { b += 1; continue; }
@@ -806,7 +830,7 @@ __device__ bool initialize(Px &P, int &wa, int &wb) {
                 last = la;
             }
         }
-        if (P.cd[a + last] - P.cd[a + first] < p.day_delta || nw - cnt < p.meow_size) { b += 1; continue; }
+        if (CDR(P, a + last) - CDR(P, a + first) < p.day_delta || nw - cnt < p.meow_size) { b += 1; continue; }
         if (cnt) {
             const int aa = a, bb = b;
             compact_drop(P, a, [&](int j) { return j < bb && tflag_at(L, j - aa); });
@@ -900,7 +924,7 @@ __device__ void lookforward(Px &P, int &wa, int &wb) {
     bool have = false;
     double change = 0.0;
     int nc = p.coef_min;
-    double fit_span = (double)P.cd[b - 1] - (double)P.cd[a];
+    double fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
     double comp[NB];
     double r[NB] = {0, 0, 0, 0, 0, 0, 0};
     int peek_start = b;
@@ -908,11 +932,11 @@ __device__ void lookforward(Px &P, int &wa, int &wb) {
         nc = num_coefs(p, b - a);
         peek_start = b;
         const int k = P.peek;
-        const double model_span = (double)P.cd[b - 1] - (double)P.cd[a];
+        const double model_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
         if (!have || b - a < 24) {
             fa = a;
             fb = b;
-            fit_span = (double)P.cd[b - 1] - (double)P.cd[a];
+            fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
             fit_models(P, fa, fb, nc);
             have = true;
 #pragma unroll
@@ -921,14 +945,14 @@ __device__ void lookforward(Px &P, int &wa, int &wb) {
             if (model_span >= 1.33 * fit_span) {
                 fa = a;
                 fb = b;
-                fit_span = (double)P.cd[b - 1] - (double)P.cd[a];
+                fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
                 fit_models(P, fa, fb, nc);
             }
             // find_closest_doy(period, peek.stop - 1, fit_window, 24) -> comparison rmse
             const int nf = fb - fa;
-            const int ref = P.cd[b + k - 1];
+            const int ref = CDR(P, b + k - 1);
             auto key4 = [&](int i) -> int {
-                const double d = (double)(P.cd[fa + i] - ref);
+                const double d = (double)(CDR(P, fa + i) - ref);
                 const double kk = fabs(rint(d / 365.25) * 365.25 - d);
                 return (int)(kk * 4.0 + 0.5);
             };
@@ -992,7 +1016,7 @@ __device__ void lookforward(Px &P, int &wa, int &wb) {
         const double md = lane_median(r[band], P.peek);
         if (l == band) mag_lane = md;
     }
-    emit(P, P.cd[a], P.cd[b - 1], P.cd[peek_start], b - a, change, nc, mag_lane);
+    emit(P, CDR(P, a), CDR(P, b - 1), CDR(P, peek_start), b - a, change, nc, mag_lane);
     wa = a;
     wb = b;
 }
@@ -1102,7 +1126,7 @@ __device__ int px_setup(Px &P, int chip, int pix) {
         if (km) carry = __shfl(d, 63 - __clzll(km));
         const unsigned long long k2 = bal(keep2);
         if (keep2) {
-            const int pos = m + below(k2);
+            const int pos = gidx(P, m + below(k2), n, __LINE__);
             P.cd[pos] = d;
             P.ci[pos] = (uint16_t)i;
 #pragma unroll

@@ -115,8 +115,9 @@ def test_staged_multichip_matches_single(ctx):
     ctx.run()
     st = ctx.stats()
     assert st['pixels'] == 2100 and st['segments'] > 0
+    fetched = [ctx.fetch(i) for i in range(3)]
     for i in range(3):
-        got = ctx.fetch(i)
+        got = fetched[i]
         ref = ctx.detect_batch(*chips[i])
         assert got.segments.tobytes() == ref.segments.tobytes()
         assert np.array_equal(got.mask, ref.mask)
