@@ -60,7 +60,10 @@ extern "C" {
 // kernel launchers (ccd_kernels.hip)
 int ccdk_prep(const int64_t *dates, int32_t n_chips, int32_t n_obs, double avg_days_yr,
               int32_t *order, int64_t *sdates, double *basis, void *stream);
-int ccdk_detect(const CcdDetectArgs *dev_args, int32_t grid, void *stream);
+// the detection kernel reads its arguments from a __constant__ symbol (one staged launch per
+// device at a time; the host API serialises launches per device)
+int ccdk_set_args(const CcdDetectArgs *host_args, void *stream);
+int ccdk_detect(int32_t grid, int variant, void *stream);
 int ccdk_scatter(const ccdgpu_segment *pool, const int32_t *pool_seq, int64_t n_pool,
                  const int64_t *offsets, int32_t n_pix_per_chip, ccdgpu_segment *out, void *stream);
 #ifdef __cplusplus

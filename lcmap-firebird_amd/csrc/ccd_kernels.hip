@@ -49,13 +49,21 @@ struct Lds {
     double coef[NB][8];  // [band][0..6] = w, [band][7] = intercept
     double rmse[8];
     double vario[8];
+    double comp[8];        // comparison rmse per band (change_magnitude)
+    double med1[8], med2[8];
     uint32_t mask[MAXW];   // processing mask, sorted order
     uint32_t tflag[MAXW];  // Tmask outlier flags of the current window
+    int sel[32];           // compacted indices of the 24 closest-DOY observations
+    double tchol[5][5];    // Tmask: Cholesky factor of the unweighted normal matrix
 };
 
+// Launch arguments live in constant memory (uniform scalar loads from every device function);
+// the per-wave LDS block is the dynamic shared segment (so every access is a ds_* instruction).
+__constant__ CcdDetectArgs c_args;
+extern __shared__ __attribute__((aligned(16))) char ccd_smem[];
+__device__ __forceinline__ Lds &LDS() { return *reinterpret_cast<Lds *>(ccd_smem); }
+
 struct Px {
-    const CcdDetectArgs *A;
-    Lds *L;
     int n;      // observations (sorted)
     int m;      // current compacted period length
     int peek;   // (adaptive) peek size
@@ -71,19 +79,18 @@ struct Px {
     unsigned long long fits, sweeps;
     unsigned long long fl;       // counted FP64 flops, wave-uniform part
     unsigned long long fl_lane;  // counted FP64 flops, per-lane part (coordinate descent)
+    mutable int bad;             // source line of a tripped index guard (0 = none), per lane
 };
 
 // ------------------------------------------------------------------ index guards
 // Every read of the compacted period goes through these: an out-of-range index is clamped (so a
-// logic error can never fault the GPU) and the first offending source line is recorded in
-// counters[4]; the host turns a nonzero value into CCDGPU_EHIP with that line number.
-__device__ __noinline__ void ccd_flag(const Px &P, int line) {
-    atomicCAS(&P.A->counters[4], 0ull, (unsigned long long)line);
-}
+// logic error can never fault the GPU) and the offending source line is kept in a register
+// (P.bad); at the end of the pixel the wave publishes it to counters[4], which the host turns
+// into CCDGPU_EHIP naming the line.
 __device__ __forceinline__ int gidx(const Px &P, int j, int lim, int line) {
-    if ((unsigned)j < (unsigned)lim) return j;
-    ccd_flag(P, line);
-    return 0;
+    const bool ok = (unsigned)j < (unsigned)lim;
+    P.bad = ok ? P.bad : line;
+    return ok ? j : 0;
 }
 __device__ __forceinline__ int32_t cdr(const Px &P, int j, int line) { return P.cd[gidx(P, j, P.m, line)]; }
 __device__ __forceinline__ int cir(const Px &P, int j, int line) {
@@ -197,7 +204,7 @@ __device__ int compact_drop(Px &P, int a, F drop) {
             dr = drop(j);
         }
         const unsigned long long keep = bal(in && !dr);
-        if (in && dr) atomicAnd(&P.L->mask[c >> 5], ~(1u << (c & 31)));
+        if (in && dr) atomicAnd(&LDS().mask[c >> 5], ~(1u << (c & 31)));
         if (in && !dr) {
             const int pos = gidx(P, out + below(keep), P.n, __LINE__);
             P.cd[pos] = d;
@@ -219,7 +226,7 @@ __device__ __forceinline__ void stage_rows(const Px &P, int j0, int cnt) {
     if (l < cnt) {
         const int j = j0 + l;
         const double *bs = P.basis + (size_t)CIR(P, j) * CCD_BASIS_STRIDE;
-        double *r = P.L->row[l];
+        double *r = LDS().row[l];
         r[0] = (double)CDR(P, j);
 #pragma unroll
         for (int c = 1; c < 7; ++c) r[c] = bs[c];
@@ -229,52 +236,73 @@ __device__ __forceinline__ void stage_rows(const Px &P, int j0, int cnt) {
     wsync();
 }
 
-// sklearn 0.18 enet_coordinate_descent (beta = 0, cyclic) in Gram form for PC active columns.
-template <int PC>
-__device__ int cd_gram(const Lds *L, int band, double alpha, int max_iter, double tol, double *wout) {
-    double g[PC][PC], q[PC], w[PC];
+// 8-lane group reductions (a band's lanes 8b .. 8b+7); results identical in all 8 lanes.
+__device__ __forceinline__ double gsum8(double v) {
+    v += __shfl_xor(v, 1);
+    v += __shfl_xor(v, 2);
+    v += __shfl_xor(v, 4);
+    return v;
+}
+__device__ __forceinline__ double gmax8(double v) {
+    double t = __shfl_xor(v, 1);
+    v = t > v ? t : v;
+    t = __shfl_xor(v, 2);
+    v = t > v ? t : v;
+    t = __shfl_xor(v, 4);
+    return t > v ? t : v;
+}
+
+// sklearn 0.18 enet_coordinate_descent (beta = 0, cyclic, duality-gap stop) in Gram form,
+// 7 bands at once: lane = band * 8 + coordinate.  Lane (b, k) holds Gram column k, q_k = Xc_k.yc_b
+// and w_k; the partial sum of coordinate j's update is an 8-lane butterfly.  Writes
+// L->coef[b][0..6]; returns the sweep count (every lane of the band's group).
+__device__ int cd_lanes(Lds *L, int pc, double alpha, int max_iter, double tol) {
+    const int l = lane();
+    const int b = l >> 3, k = l & 7;
+    const bool act = b < NB && k < pc;
+    double gcol[7];
 #pragma unroll
-    for (int j = 0; j < PC; ++j) {
-        q[j] = L->Q[j][band];
-        w[j] = 0.0;
-#pragma unroll
-        for (int k = 0; k < PC; ++k) g[j][k] = L->G[j][k];
-    }
-    const double yy = L->YY[band];
-    const double d_w_tol = tol;
+    for (int j = 0; j < 7; ++j) gcol[j] = (act && j < pc) ? L->G[j][k] : 0.0;
+    const double gkk = act ? L->G[k][k] : 0.0;
+    const double q = act ? L->Q[k][b] : 0.0;
+    const double yy = b < NB ? L->YY[b] : 0.0;
     const double tol_s = tol * yy;
-    int it = 0;
-    for (it = 0; it < max_iter; ++it) {
-        double w_max = 0.0, d_w_max = 0.0;
+    double w = 0.0;
+    bool done = b >= NB;
+    int sweeps = max_iter;
+    for (int it = 0; it < max_iter; ++it) {
+        if (bal(!done) == 0ull) break;
+        double dl = 0.0;
 #pragma unroll
-        for (int j = 0; j < PC; ++j) {
-            if (g[j][j] == 0.0) continue;
-            double tmp = q[j];
-#pragma unroll
-            for (int k = 0; k < PC; ++k)
-                if (k != j) tmp -= g[j][k] * w[k];
-            const double aa = fabs(tmp) - alpha;
-            const double wn = aa > 0.0 ? (tmp > 0.0 ? aa : -aa) / g[j][j] : 0.0;
-            const double d = fabs(wn - w[j]);
-            w[j] = wn;
-            d_w_max = d > d_w_max ? d : d_w_max;
-            w_max = fabs(wn) > w_max ? fabs(wn) : w_max;
-        }
-        if (w_max == 0.0 || d_w_max / w_max < d_w_tol || it == max_iter - 1) {
-            double dual = 0.0, wq = 0.0, wxta = 0.0, l1 = 0.0;
-#pragma unroll
-            for (int j = 0; j < PC; ++j) {
-                double gw = 0.0;
-#pragma unroll
-                for (int k = 0; k < PC; ++k) gw += g[j][k] * w[k];
-                const double xta = q[j] - gw;
-                dual = fabs(xta) > dual ? fabs(xta) : dual;
-                wq += w[j] * q[j];
-                wxta += w[j] * xta;
-                l1 += fabs(w[j]);
+        for (int j = 0; j < 7; ++j) {
+            if (j >= pc) break;
+            const double s = gsum8((act && k != j) ? gcol[j] * w : 0.0);
+            if (act && !done && k == j && gkk != 0.0) {
+                const double tmp = q - s;
+                const double aa = fabs(tmp) - alpha;
+                const double wn = aa > 0.0 ? (tmp > 0.0 ? aa : -aa) / gkk : 0.0;
+                dl = fabs(wn - w);
+                w = wn;
             }
-            const double ry = yy - wq;        // R . y
-            const double rr = ry - wxta;      // R . R = yy - 2 w.q + w.G.w
+        }
+        const double d_w_max = gmax8(dl);
+        const double w_max = gmax8(act ? fabs(w) : 0.0);
+        const bool check = !done && (w_max == 0.0 || d_w_max / w_max < tol || it == max_iter - 1);
+        if (bal(check)) {
+            double gw = 0.0;
+#pragma unroll
+            for (int kk = 0; kk < 7; ++kk) {
+                if (kk >= pc) break;
+                const double t = gsum8(act ? gcol[kk] * w : 0.0);
+                if (k == kk) gw = t;
+            }
+            const double xta = act ? q - gw : 0.0;
+            const double dual = gmax8(fabs(xta));
+            const double wq = gsum8(w * q);
+            const double wxta = gsum8(w * xta);
+            const double l1 = gsum8(fabs(w));
+            const double ry = yy - wq;    // R . y
+            const double rr = ry - wxta;  // R . R = yy - 2 w.q + w.G.w
             double cst, gap;
             if (dual > alpha) {
                 cst = alpha / dual;
@@ -284,18 +312,31 @@ __device__ int cd_gram(const Lds *L, int band, double alpha, int max_iter, doubl
                 gap = rr;
             }
             gap += alpha * l1 - cst * ry;
-            if (gap < tol_s) break;
+            if (check && gap < tol_s) {
+                done = true;
+                sweeps = it + 1;
+            }
         }
     }
+    if (b < NB && k < 7) L->coef[b][k] = act ? w : 0.0;
+    return sweeps;
+}
+
+// residual of band b at compacted observation j for the current models (lasso.predict)
+__device__ __forceinline__ double resid_at(const Px &P, int band, int j) {
+    const double *bs = P.basis + (size_t)CIR(P, j) * CCD_BASIS_STRIDE;
+    const double *c = LDS().coef[band];
+    double pr = (double)CDR(P, j) * c[0];
 #pragma unroll
-    for (int j = 0; j < PC; ++j) wout[j] = w[j];
-    return (it < max_iter ? it : max_iter - 1) + 1;
+    for (int jj = 1; jj < 7; ++jj) pr += bs[jj] * c[jj];
+    pr += c[7];
+    return cvalf(P, band, j) - pr;
 }
 
 // lasso.fitted_model for the 7 bands over compacted window [a, b) with k coefficients.
 __device__ void fit_models(Px &P, int a, int b, int k) {
-    const ccdgpu_params &p = P.A->p;
-    Lds *L = P.L;
+    const ccdgpu_params &p = c_args.p;
+    Lds *L = &LDS();
     const int l = lane();
     const int nw = b - a;
     const int pc = k - 1;  // active design columns (t + harmonics)
@@ -367,71 +408,47 @@ __device__ void fit_models(Px &P, int a, int b, int k) {
         }
     }
     wsync();
-    // coordinate descent, lane = band
-    if (l < NB) {
-        double w[7] = {0, 0, 0, 0, 0, 0, 0};
-        const double alpha = p.lasso_alpha * nw;
-        int sw;
-        if (pc == 3) sw = cd_gram<3>(L, l, alpha, p.lasso_max_iter, p.lasso_tol, w);
-        else if (pc == 5) sw = cd_gram<5>(L, l, alpha, p.lasso_max_iter, p.lasso_tol, w);
-        else sw = cd_gram<7>(L, l, alpha, p.lasso_max_iter, p.lasso_tol, w);
-        double dot = 0.0;
-#pragma unroll
-        for (int j = 0; j < 7; ++j) {
-            dot += L->xm[j] * w[j];
-            L->coef[l][j] = w[j];
-        }
-        L->coef[l][7] = L->ym[l] - dot;
+    // coordinate descent: lane = band * 8 + coordinate
+    const int sw = cd_lanes(L, pc, p.lasso_alpha * nw, p.lasso_max_iter, p.lasso_tol);
+    if ((l & 7) == 0 && (l >> 3) < NB) {
         P.sweeps += (unsigned long long)sw;  // per-lane; reduced at the end
         P.fl_lane += (unsigned long long)sw * (unsigned long long)(2 * pc * pc + 6 * pc) + 14;
+    }
+    wsync();
+    if (l < NB) {
+        double dot = 0.0;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) dot += L->xm[j] * L->coef[l][j];
+        L->coef[l][7] = L->ym[l] - dot;
     }
     P.fits += NB;
     // means 14 n, centred Gram/X'y entries 4 n each, rmse 7 * (2*7 + 3) n
     P.fl += (unsigned long long)nw * (unsigned long long)(14 + 4 * nE + 7 * 17) + 14;
     wsync();
-    // rmse from residuals of the raw design (predict = X @ coef + intercept)
-    double ss[NB] = {0, 0, 0, 0, 0, 0, 0};
-    for (int t0 = 0; t0 < nw; t0 += W) {
-        const int j = a + t0 + l;
-        if (t0 + l < nw) {
-            const double *bs = P.basis + (size_t)CIR(P, j) * CCD_BASIS_STRIDE;
-            const double x0 = (double)CDR(P, j);
-#pragma unroll
-            for (int band = 0; band < NB; ++band) {
-                const double *c = L->coef[band];
-                double pr = x0 * c[0];
-#pragma unroll
-                for (int jj = 1; jj < 7; ++jj) pr += bs[jj] * c[jj];
-                pr += c[7];
-                const double r = cvalf(P, band, j) - pr;
-                ss[band] += r * r;
+    // rmse from residuals of the raw design (predict = X @ coef + intercept);
+    // lane = (observation sub-index, band), 8 observations per pass
+    {
+        const int bnd = l & 7, osub = l >> 3;
+        double ss = 0.0;
+        if (bnd < NB)
+            for (int t0 = osub; t0 < nw; t0 += 8) {
+                const double r = resid_at(P, bnd, a + t0);
+                ss += r * r;
             }
-        }
-    }
-    const double den = (double)(nw - (p.rmse_dof ? k : 0));
-#pragma unroll
-    for (int band = 0; band < NB; ++band) {
-        const double t = wsum(ss[band]);
-        if (l == 0) L->rmse[band] = sqrt(t / den);
+        ss += __shfl_xor(ss, 8);
+        ss += __shfl_xor(ss, 16);
+        ss += __shfl_xor(ss, 32);
+        const double den = (double)(nw - (p.rmse_dof ? k : 0));
+        if (l < NB) L->rmse[l] = sqrt(ss / den);
     }
     wsync();
 }
 
-// residual of band b at compacted observation j for the current models (lasso.predict)
-__device__ __forceinline__ double resid_at(const Px &P, int band, int j) {
-    const double *bs = P.basis + (size_t)CIR(P, j) * CCD_BASIS_STRIDE;
-    const double *c = P.L->coef[band];
-    double pr = (double)CDR(P, j) * c[0];
-#pragma unroll
-    for (int jj = 1; jj < 7; ++jj) pr += bs[jj] * c[jj];
-    pr += c[7];
-    return cvalf(P, band, j) - pr;
-}
 
 // ------------------------------------------------------------------ segment output
 __device__ void emit(Px &P, int sday, int eday, int bday, int count, double chprob, int cqa,
                      double mag_lane /* lane b: magnitude of band b */) {
-    const CcdDetectArgs &A = *P.A;
+    const CcdDetectArgs &A = c_args;
     const int l = lane();
     unsigned long long slot = 0;
     if (l == 0) slot = atomicAdd(&A.counters[1], 1ull);
@@ -444,10 +461,10 @@ __device__ void emit(Px &P, int sday, int eday, int bday, int count, double chpr
     ccdgpu_segment *s = A.pool + slot;
     if (l < NB) {
         s->magnitude[l] = mag_lane;
-        s->rmse[l] = P.L->rmse[l];
-        s->intercept[l] = P.L->coef[l][7];
+        s->rmse[l] = LDS().rmse[l];
+        s->intercept[l] = LDS().coef[l][7];
 #pragma unroll
-        for (int j = 0; j < 7; ++j) s->coef[l][j] = P.L->coef[l][j];
+        for (int j = 0; j < 7; ++j) s->coef[l][j] = LDS().coef[l][j];
     }
     if (l == 0) {
         s->start_day = sday;
@@ -463,14 +480,14 @@ __device__ void emit(Px &P, int sday, int eday, int bday, int count, double chpr
 }
 
 __device__ void catch_(Px &P, int a, int b, int cqa) {
-    fit_models(P, a, b, P.A->p.coef_min);
+    fit_models(P, a, b, c_args.p.coef_min);
     const int bday = b < P.m ? CDR(P, b) : CDR(P, P.m - 1);
     emit(P, CDR(P, a), CDR(P, b - 1), bday, b - a, 0.0, cqa, 0.0);
 }
 
 // ------------------------------------------------------------------ variogram / peek
 __device__ void variogram(Px &P) {
-    Lds *L = P.L;
+    Lds *L = &LDS();
     const int l = lane();
     const int m = P.m;
     if (m < 2) {
@@ -511,7 +528,7 @@ __device__ void variogram(Px &P) {
 }
 
 __device__ void adjust_peek(Px &P) {
-    const ccdgpu_params &p = P.A->p;
+    const ccdgpu_params &p = c_args.p;
     P.peek = p.peek_size;
     P.chg = p.change_threshold;
     if (!p.adaptive_peek || P.m < 2) return;
@@ -523,212 +540,243 @@ __device__ void adjust_peek(Px &P) {
     const double adj = rint((double)(p.peek_size * 16) / delta);
     if (adj > (double)p.peek_size) {
         P.peek = adj > (double)CCDGPU_MAX_PEEK ? CCDGPU_MAX_PEEK : (int)adj;
-        P.chg = P.A->thr_table[P.peek];
+        P.chg = c_args.thr_table[P.peek];
     }
 }
 
 // ------------------------------------------------------------------ Tmask (models/tmask.py + robust_fit.py)
-// Cholesky solve of an n x n SPD system (n <= 5), redundantly in every lane (uniform result).
-__device__ bool chol5(double (&a)[5][5], int n) {
-    for (int j = 0; j < n; ++j) {
+// Tmask design row: [cos wt, sin wt, cos (w/N) t, sin (w/N) t, 1]; when N = 1 the annual and the
+// observation cycle coincide (rank-deficient 5-column design) and the row is [cos, sin, 1, 0, 0]
+// with the two unused normal-matrix diagonals pinned to 1 (Tmask).
+__device__ __forceinline__ void tm_row(const Px &P, int j, int i, int ncol, const double *xoc,
+                                       const double *xos, double (&x)[5]) {
+    const double *bs = P.basis + (size_t)CIR(P, j) * CCD_BASIS_STRIDE;
+    x[0] = bs[1];
+    x[1] = bs[2];
+    if (ncol == 5) {
+        x[2] = xoc[i];
+        x[3] = xos[i];
+        x[4] = 1.0;
+    } else {
+        x[2] = 1.0;
+        x[3] = 0.0;
+        x[4] = 0.0;
+    }
+}
+
+// normal equations sum w x x^T and sum w x y over the window into L->G[0..4][0..4] and
+// L->Q[0..4][0]: rows [x0..x4, w, y] staged in LDS 64 at a time, lane = matrix entry,
+// sequential over rows (same scheme as the Lasso Gram in fit_models).
+__device__ void tm_normal(const Px &P, int a, int nw, int ncol, const double *xoc,
+                                       const double *xos, int band, const double *wv) {
+    Lds *L = &LDS();
+    const int l = lane();
+    int ea = -1, eb = -1;
+    if (l < 15) {
+        int e = l, r = 0;
+        while (e > r) { e -= r + 1; ++r; }
+        ea = r;
+        eb = e;
+    } else if (l < 20) {
+        ea = l - 15;
+        eb = 6;
+    }
+    double acc = 0.0;
+    for (int t0 = 0; t0 < nw; t0 += W) {
+        const int cnt = nw - t0 < W ? nw - t0 : W;
+        if (l < cnt) {
+            const int i = t0 + l;
+            double x[5];
+            tm_row(P, a + i, i, ncol, xoc, xos, x);
+            double *row = L->row[l];
+#pragma unroll
+            for (int r = 0; r < 5; ++r) row[r] = x[r];
+            row[5] = wv ? wv[i] : 1.0;
+            row[6] = band >= 0 ? cvalf(P, band, a + i) : 0.0;
+        }
+        wsync();
+        if (ea >= 0)
+            for (int r = 0; r < cnt; ++r) acc += L->row[r][5] * L->row[r][ea] * L->row[r][eb];
+        wsync();
+    }
+    if (l < 15) {
+        L->G[ea][eb] = acc;
+        L->G[eb][ea] = acc;
+    } else if (l < 20) {
+        L->Q[ea][0] = acc;
+    }
+    wsync();
+    if (ncol == 3 && l == 0) {
+        L->G[3][3] = 1.0;
+        L->G[4][4] = 1.0;
+    }
+    wsync();
+}
+
+__device__ __forceinline__ void tm_load(const Lds *L, double (&A)[5][5], double (&rhs)[5]) {
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+        rhs[r] = L->Q[r][0];
+#pragma unroll
+        for (int c = 0; c < 5; ++c) A[r][c] = L->G[r][c];
+    }
+}
+
+// in-place lower Cholesky factor of a 5x5 SPD matrix; false if not positive definite
+__device__ __forceinline__ bool chol5(double (&a)[5][5]) {
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
         double d = a[j][j];
+#pragma unroll
         for (int k = 0; k < j; ++k) d -= a[j][k] * a[j][k];
         if (!(d > 0.0)) return false;
         d = sqrt(d);
         a[j][j] = d;
-        for (int i = j + 1; i < n; ++i) {
+#pragma unroll
+        for (int i = j + 1; i < 5; ++i) {
             double s = a[i][j];
+#pragma unroll
             for (int k = 0; k < j; ++k) s -= a[i][k] * a[j][k];
             a[i][j] = s / d;
         }
     }
     return true;
 }
-__device__ void chol_solve(const double (&c)[5][5], int n, const double *b, double *x) {
+__device__ __forceinline__ void chol5_solve(const double (&c)[5][5], const double (&b)[5], double (&x)[5]) {
     double z[5];
-    for (int i = 0; i < n; ++i) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
         double s = b[i];
+#pragma unroll
         for (int k = 0; k < i; ++k) s -= c[i][k] * z[k];
         z[i] = s / c[i][i];
     }
-    for (int i = n - 1; i >= 0; --i) {
+#pragma unroll
+    for (int i = 4; i >= 0; --i) {
         double s = z[i];
-        for (int k = i + 1; k < n; ++k) s -= c[k][i] * x[k];
+#pragma unroll
+        for (int k = i + 1; k < 5; ++k) s -= c[k][i] * x[k];
         x[i] = s / c[i][i];
     }
 }
 
-// weighted normal equations sum_i w_i x_i x_i^T, sum_i w_i x_i y_i over the window (lane = obs).
-// x rows: [c1, s1, (cos oc t, sin oc t), 1]; weights from wv (nullptr = 1).
-__device__ bool tm_solve(const Px &P, int a, int nw, int ncol, const double *xoc, const double *xos,
-                         int band, const double *wv, double *coef) {
-    const int l = lane();
-    double acc[20];
+// solve with a fallback for a (numerically) singular weighted system: zero coefficients
+__device__ __forceinline__ void tm_solve(double (&A)[5][5], const double (&rhs)[5], double (&coef)[5]) {
+    if (chol5(A)) {
+        chol5_solve(A, rhs, coef);
+    } else {
 #pragma unroll
-    for (int e = 0; e < 20; ++e) acc[e] = 0.0;
-    for (int t0 = 0; t0 < nw; t0 += W) {
-        const int i = t0 + l;
-        if (i < nw) {
-            const double *bs = P.basis + (size_t)CIR(P, a + i) * CCD_BASIS_STRIDE;
-            double x[5];
-            x[0] = bs[1];
-            x[1] = bs[2];
-            if (ncol == 5) { x[2] = xoc[i]; x[3] = xos[i]; x[4] = 1.0; }
-            else { x[2] = 1.0; x[3] = 0.0; x[4] = 0.0; }
-            const double wt = wv ? wv[i] : 1.0;
-            const double y = cvalf(P, band, a + i);
-            int e = 0;
-#pragma unroll
-            for (int r = 0; r < 5; ++r) {
-#pragma unroll
-                for (int c = 0; c <= r; ++c) acc[e++] += wt * x[r] * x[c];
-            }
-#pragma unroll
-            for (int r = 0; r < 5; ++r) acc[15 + r] += wt * x[r] * y;
-        }
-    }
-    double A[5][5], rhs[5];
-    int e = 0;
-#pragma unroll
-    for (int r = 0; r < 5; ++r) {
-#pragma unroll
-        for (int c = 0; c <= r; ++c) {
-            const double v = wsum(acc[e++]);
-            A[r][c] = v;
-            A[c][r] = v;
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < 5; ++r) rhs[r] = wsum(acc[15 + r]);
-    if (!chol5(A, ncol)) {
         for (int r = 0; r < 5; ++r) coef[r] = 0.0;
-        return false;
     }
-    chol_solve(A, ncol, rhs, coef);
-    for (int r = ncol; r < 5; ++r) coef[r] = 0.0;
-    return true;
 }
 
-__device__ __forceinline__ double tm_pred(const Px &P, int j, int ncol, double xc, double xs, const double *coef) {
-    const double *bs = P.basis + (size_t)CIR(P, j) * CCD_BASIS_STRIDE;
-    double pr = bs[1] * coef[0] + bs[2] * coef[1];
-    if (ncol == 5) pr += xc * coef[2] + xs * coef[3] + coef[4];
-    else pr += coef[2];
+__device__ __forceinline__ double tm_pred(const Px &P, int j, int i, int ncol, const double *xoc,
+                                          const double *xos, const double (&coef)[5]) {
+    double x[5];
+    tm_row(P, j, i, ncol, xoc, xos, x);
+    double pr = 0.0;
+#pragma unroll
+    for (int r = 0; r < 5; ++r) pr += x[r] * coef[r];
     return pr;
+}
+
+// cos / sin of the observation-cycle harmonic (w / N) t for the window (lane = obs)
+__device__ void tm_trig(const Px &P, int a, int nw, double oc, double *xoc, double *xos) {
+    for (int i = lane(); i < nw; i += W) {
+        double sv, cv;
+        sincos(oc * (double)CDR(P, a + i), &sv, &cv);
+        xoc[i] = cv;
+        xos[i] = sv;
+    }
 }
 
 // Returns the outlier count; outlier flags in L->tflag (bit i = window observation i).
 __device__ int tmask(Px &P, int a, int b) {
-    const ccdgpu_params &p = P.A->p;
-    Lds *L = P.L;
+    const ccdgpu_params &p = c_args.p;
+    Lds *L = &LDS();
     const int l = lane();
     const int nw = b - a;
     const double w = 2.0 * M_PI / p.avg_days_yr;
     const double oc = w / ceil(((double)CDR(P, b - 1) - (double)CDR(P, a)) / p.avg_days_yr);
     const int ncol = (oc == w) ? 3 : 5;
-    // leverage + Gram (45 n) + per band: stats 4 n, OLS 60 n, <= 4 IRLS passes of 60 n + 18 n
     P.fl += (unsigned long long)nw * (2 + 45 + 25);
     double *xoc = P.fs, *xos = P.fs + P.n, *adj = P.fs + 2 * P.n, *absr = P.fs + 3 * P.n,
            *wt = P.fs + 4 * P.n;
-    // observation-cycle harmonics and flags
-    for (int t0 = 0; t0 < nw; t0 += W) {
-        const int i = t0 + l;
-        if (i < nw && ncol == 5) {
-            const double t = (double)CDR(P, a + i);
-            double sv, cv;
-            sincos(oc * t, &sv, &cv);
-            xoc[i] = cv;
-            xos[i] = sv;
-        }
-    }
+    if (ncol == 5) tm_trig(P, a, nw, oc, xoc, xos);
     for (int i = l; i < (nw + 31) / 32; i += W) L->tflag[i] = 0u;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     wsync();
-    // leverage from the unweighted normal matrix (robust_fit.RLM: h = diag(X (X'X)^-1 X'))
-    double G0[5][5];
+    // unweighted normal matrix: OLS solves and leverage h = diag(X (X'X)^-1 X') (robust_fit.RLM);
+    // its Cholesky factor is kept in LDS (L->tchol) for the per-band OLS solves
+    bool ok0;
     {
-        double acc[15];
+        double G0[5][5], rhs0[5];
+        tm_normal(P, a, nw, ncol, xoc, xos, -1, nullptr);
+        tm_load(&LDS(), G0, rhs0);
+        ok0 = chol5(G0);
+        if (l == 0)
 #pragma unroll
-        for (int e = 0; e < 15; ++e) acc[e] = 0.0;
-        for (int t0 = 0; t0 < nw; t0 += W) {
-            const int i = t0 + l;
-            if (i < nw) {
-                const double *bs = P.basis + (size_t)CIR(P, a + i) * CCD_BASIS_STRIDE;
-                double x[5] = {bs[1], bs[2], ncol == 5 ? xoc[i] : 1.0, ncol == 5 ? xos[i] : 0.0,
-                               ncol == 5 ? 1.0 : 0.0};
-                int e = 0;
+            for (int r = 0; r < 5; ++r)
 #pragma unroll
-                for (int r = 0; r < 5; ++r)
-#pragma unroll
-                    for (int c = 0; c <= r; ++c) acc[e++] += x[r] * x[c];
-            }
-        }
-        int e = 0;
-#pragma unroll
-        for (int r = 0; r < 5; ++r)
-#pragma unroll
-            for (int c = 0; c <= r; ++c) {
-                const double v = wsum(acc[e++]);
-                G0[r][c] = v;
-                G0[c][r] = v;
-            }
-        const bool ok = chol5(G0, ncol);
-        for (int t0 = 0; t0 < nw; t0 += W) {
-            const int i = t0 + l;
-            if (i < nw) {
-                const double *bs = P.basis + (size_t)CIR(P, a + i) * CCD_BASIS_STRIDE;
-                double x[5] = {bs[1], bs[2], ncol == 5 ? xoc[i] : 1.0, ncol == 5 ? xos[i] : 0.0, 1.0};
-                double h = 0.9999;
-                if (ok) {
-                    double z[5], hh = 0.0;
-                    for (int r = 0; r < ncol; ++r) {
-                        double s = x[r];
-                        for (int k = 0; k < r; ++k) s -= G0[r][k] * z[k];
-                        z[r] = s / G0[r][r];
-                        hh += z[r] * z[r];
-                    }
-                    h = hh < 0.9999 ? hh : 0.9999;
-                }
-                adj[i] = 1.0 / sqrt(1.0 - h);
-            }
-        }
+                for (int c = 0; c < 5; ++c) L->tchol[r][c] = G0[r][c];
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     wsync();
+    for (int i = l; i < nw; i += W) {
+        double x[5];
+        tm_row(P, a + i, i, ncol, xoc, xos, x);
+        double h = 0.9999;
+        if (ok0) {
+            double z[5], hh = 0.0;
+#pragma unroll
+            for (int r = 0; r < 5; ++r) {
+                double s2 = x[r];
+#pragma unroll
+                for (int k = 0; k < r; ++k) s2 -= L->tchol[r][k] * z[k];
+                z[r] = s2 / L->tchol[r][r];
+                hh += z[r] * z[r];
+            }
+            h = hh < 0.9999 ? hh : 0.9999;
+        }
+        adj[i] = 1.0 / sqrt(1.0 - h);
+    }
     for (int band = 0; band < NB; ++band) {
         if (!((p.tmask_bands >> band) & 1u)) continue;
         // y statistics (np.std, population)
         double sy = 0.0;
-        for (int t0 = 0; t0 < nw; t0 += W)
-            if (t0 + l < nw) sy += cvalf(P, band, a + t0 + l);
+        for (int i = l; i < nw; i += W) sy += cvalf(P, band, a + i);
         const double ym = wsum(sy) / nw;
         double sv = 0.0;
-        for (int t0 = 0; t0 < nw; t0 += W)
-            if (t0 + l < nw) {
-                const double d = cvalf(P, band, a + t0 + l) - ym;
-                sv += d * d;
-            }
+        for (int i = l; i < nw; i += W) {
+            const double d = cvalf(P, band, a + i) - ym;
+            sv += d * d;
+        }
         const double ystd = sqrt(wsum(sv) / nw);
         double coef[5], coef0[5];
-        tm_solve(P, a, nw, ncol, xoc, xos, band, nullptr, coef);
+        {
+            double Gt[5][5], r0[5];
+            tm_normal(P, a, nw, ncol, xoc, xos, band, nullptr);
+            tm_load(&LDS(), Gt, r0);
+            if (ok0) {
+#pragma unroll
+                for (int r = 0; r < 5; ++r)
+#pragma unroll
+                    for (int c = 0; c < 5; ++c) Gt[r][c] = L->tchol[r][c];
+                chol5_solve(Gt, r0, coef);
+            } else {
+                tm_solve(Gt, r0, coef);
+            }
+        }
         P.fl += (unsigned long long)nw * (4 + 60 + 12) + 120;
         int iteration = 1;
         bool converged = false;
         while (!converged && iteration < 5) {
 #pragma unroll
             for (int r = 0; r < 5; ++r) coef0[r] = coef[r];
-            for (int t0 = 0; t0 < nw; t0 += W) {
-                const int i = t0 + l;
-                if (i < nw) {
-                    const double r = (cvalf(P, band, a + i) -
-                                      tm_pred(P, a + i, ncol, ncol == 5 ? xoc[i] : 0.0, ncol == 5 ? xos[i] : 0.0, coef0)) *
-                                     adj[i];
-                    wt[i] = r;  // signed, adjusted residual
-                    absr[i] = fabs(r);
-                }
+            for (int i = l; i < nw; i += W) {
+                const double r = (cvalf(P, band, a + i) - tm_pred(P, a + i, i, ncol, xoc, xos, coef0)) * adj[i];
+                wt[i] = r;  // signed, adjusted residual
+                absr[i] = fabs(r);
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            wsync();
             // mad = median(sort(|r|)[4:]) / 0.6745
             const int c = nw - 4;
             double med;
@@ -737,18 +785,16 @@ __device__ int tmask(Px &P, int a, int b) {
             const double mad = med / 0.6745;
             const double floor_ = 2.220446049250313e-16 * ystd;
             const double scale = mad > floor_ ? mad : floor_;
-            for (int t0 = 0; t0 < nw; t0 += W) {
-                const int i = t0 + l;
-                if (i < nw) {
-                    const double u = wt[i] / scale;
-                    const double q = u / 4.685;
-                    const double om = 1.0 - q * q;
-                    wt[i] = fabs(u) < 4.685 ? om * om : 0.0;
-                }
+            for (int i = l; i < nw; i += W) {
+                const double u = wt[i] / scale;
+                const double q = u / 4.685;
+                const double om = 1.0 - q * q;
+                wt[i] = fabs(u) < 4.685 ? om * om : 0.0;
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            wsync();
-            tm_solve(P, a, nw, ncol, xoc, xos, band, wt, coef);
+            double Gw[5][5], rw[5];
+            tm_normal(P, a, nw, ncol, xoc, xos, band, wt);
+            tm_load(&LDS(), Gw, rw);
+            tm_solve(Gw, rw, coef);
             P.fl += (unsigned long long)nw * (60 + 18) + 120;
             iteration += 1;
             converged = true;
@@ -761,7 +807,7 @@ __device__ int tmask(Px &P, int a, int b) {
             const int i = t0 + l;
             bool out = false;
             if (i < nw) {
-                const double pr = tm_pred(P, a + i, ncol, ncol == 5 ? xoc[i] : 0.0, ncol == 5 ? xos[i] : 0.0, coef) + 0.0;
+                const double pr = tm_pred(P, a + i, i, ncol, xoc, xos, coef) + 0.0;
                 out = fabs(pr - cvalf(P, band, a + i)) > thr;
             }
             const unsigned long long bm = bal(out);
@@ -790,8 +836,8 @@ __device__ __forceinline__ int num_coefs(const ccdgpu_params &p, int n) {
 }
 
 __device__ bool stable(const Px &P, int a, int b) {
-    const ccdgpu_params &p = P.A->p;
-    const Lds *L = P.L;
+    const ccdgpu_params &p = c_args.p;
+    const Lds *L = &LDS();
     const int l = lane();
     double v2 = 0.0;
     if (l < NB && ((p.detection_bands >> l) & 1u)) {
@@ -807,8 +853,8 @@ __device__ bool stable(const Px &P, int a, int b) {
 __device__ __forceinline__ void count_stable(Px &P) { P.fl += 5 * (2 * 16 + 8) + 6; }
 
 __device__ bool initialize(Px &P, int &wa, int &wb) {
-    const ccdgpu_params &p = P.A->p;
-    const Lds *L = P.L;
+    const ccdgpu_params &p = c_args.p;
+    const Lds *L = &LDS();
     const int l = lane();
     int a = wa, b = wb;
     bool ok = false;
@@ -847,46 +893,83 @@ __device__ bool initialize(Px &P, int &wa, int &wb) {
     return ok;
 }
 
-// change magnitude of the lane's peek residuals (only detection bands)
-__device__ __forceinline__ double magnitude(const Px &P, const double (&r)[NB], const double *comp) {
-    const ccdgpu_params &p = P.A->p;
-    double s = 0.0;
-#pragma unroll
-    for (int band = 0; band < NB; ++band) {
-        if (!((p.detection_bands >> band) & 1u)) continue;
-        const double vr = P.L->vario[band];
-        const double cr = comp[band];
-        const double rm = (vr != vr || cr != cr) ? __builtin_nan("") : (vr > cr ? vr : cr);
-        const double v = r[band] / rm;
-        s += v * v;
+// Peek evaluation shared by lookback and lookforward: lane = (peek observation jj, band),
+// 8 observations per pass, jj = pass * 8 + (lane >> 3).  Residuals of the current models
+// (lasso.predict), change magnitude = sum over detection bands of (r / max(vario, comp))^2
+// (change.change_magnitude) reduced over the 8 band lanes.  rl[pass] keeps each lane's residual
+// for the segment's magnitude medians.  Returns true iff every peek observation exceeds the
+// change threshold (change.detect_change); mag0 = magnitude of observation 0 (detect_outlier).
+__device__ bool eval_peek(Px &P, int k, int start, int dir, double &mag0) {
+    const ccdgpu_params &p = c_args.p;
+    Lds *L = &LDS();
+    const int l = lane();
+    const int bnd = l & 7, osub = l >> 3;
+    const bool det = bnd < NB && ((p.detection_bands >> bnd) & 1u);
+    double rm = 1.0;
+    if (bnd < NB) {
+        const double vr = L->vario[bnd], cr = L->comp[bnd];
+        rm = (vr != vr || cr != cr) ? __builtin_nan("") : (vr > cr ? vr : cr);
     }
-    return s;
+    bool all = true;
+    mag0 = 0.0;
+#pragma unroll
+    for (int pass = 0; pass < 8; ++pass) {
+        if (pass * 8 >= k) break;
+        const int jj = pass * 8 + osub;
+        const bool valid = jj < k && bnd < NB;
+        double r = 0.0;
+        if (valid) r = resid_at(P, bnd, start + dir * jj);
+        if (jj < k) L->row[jj][bnd] = r;  // kept for the segment's magnitude medians
+        const double v = r / rm;
+        const double mag = gsum8((valid && det) ? v * v : 0.0);
+        if (bal(bnd == 0 && jj < k && !(mag > P.chg))) all = false;
+        if (pass == 0) mag0 = __shfl(mag, 0);
+    }
+    P.fl += (unsigned long long)k * (7 * 16 + 5 * 4);
+    wsync();
+    return all;
+}
+
+// Median over the k peek residuals of each band (lookforward result magnitudes, taken from
+// L->row where eval_peek left them); returns band l's median in lane l (l < 7).
+__device__ double peek_medians(Px &P, int k) {
+    Lds *L = &LDS();
+    const int l = lane();
+    const int bnd = l & 7, osub = l >> 3;
+    const int t1 = (k - 1) / 2, t2 = k / 2;
+    for (int jj = osub; jj < k; jj += 8) {
+        if (bnd >= NB) continue;
+        const double v = L->row[jj][bnd];
+        int rank = 0;
+        for (int i = 0; i < k; ++i) {
+            const double u = L->row[i][bnd];
+            rank += (u < v || (u == v && i < jj)) ? 1 : 0;
+        }
+        if (rank == t1) L->med1[bnd] = v;
+        if (rank == t2) L->med2[bnd] = v;
+    }
+    wsync();
+    double out = 0.0;
+    if (l < NB) out = (k & 1) ? L->med1[l] : (L->med1[l] + L->med2[l]) / 2.0;
+    wsync();
+    return out;
 }
 
 __device__ void lookback(Px &P, int &wa, int &wb, int prev) {
-    const ccdgpu_params &p = P.A->p;
+    const ccdgpu_params &p = c_args.p;
     const int l = lane();
     int a = wa, b = wb;
-    double comp[NB];
-#pragma unroll
-    for (int band = 0; band < NB; ++band) comp[band] = P.L->rmse[band];
+    if (l < NB) LDS().comp[l] = LDS().rmse[l];  // change.lookback: comparison rmse = model rmse
+    wsync();
     while (a > prev) {
         int lo;
         if (a - prev > P.peek) lo = a - P.peek + 1;
         else if (a - P.peek <= 0) lo = 0;
         else lo = prev;
         const int k = a - lo;
-        double r[NB];
-        double mag = 0.0;
-        if (l < k) {
-#pragma unroll
-            for (int band = 0; band < NB; ++band) r[band] = resid_at(P, band, a - 1 - l);
-            mag = magnitude(P, r, comp);
-        }
-        P.fl += (unsigned long long)k * (7 * 16 + 5 * 4);
-        const bool change = bal(l < k && !(mag > P.chg)) == 0ull;
+        double m0;
+        const bool change = eval_peek(P, k, a - 1, -1, m0);
         if (change) break;
-        const double m0 = __shfl(mag, 0);
         if (m0 > p.outlier_threshold) {
             const int rm = a - 1;
             compact_drop(P, rm, [&](int j) { return j == rm; });
@@ -900,24 +983,60 @@ __device__ void lookback(Px &P, int &wa, int &wb, int prev) {
     wb = b;
 }
 
-// median over lanes [0, k) of v (per band), rank counting with shuffles
-__device__ double lane_median(double v, int k) {
+// find_closest_doy(period, ref, fit_window, 24) -> comparison rmse sqrt(sum r^2) / 4 per band
+// into L->comp.  Keys |round(d / 365.25) * 365.25 - d| are multiples of 0.25 days (integers x4),
+// selected by counting (stable argsort order: ties by index).
+__device__ void closest_doy_comp(Px &P, int fa, int fb, int ref_idx) {
+    Lds *L = &LDS();
     const int l = lane();
-    int rank = 0;
-    for (int i = 0; i < k; ++i) {
-        const double u = __shfl(v, i);
-        rank += (u < v || (u == v && i < l)) ? 1 : 0;
+    const int nf = fb - fa;
+    const int ref = CDR(P, ref_idx);
+    auto key4 = [&](int i) -> int {
+        const double d = (double)(CDR(P, fa + i) - ref);
+        const double kk = fabs(rint(d / 365.25) * 365.25 - d);
+        return (int)(kk * 4.0 + 0.5);
+    };
+    int K = 1 << 20, need = 0;
+    if (nf > 24) {
+        auto gen = [&](int i, int &v) -> bool { v = key4(i); return true; };
+        K = kth_int(gen, nf, 23, 0, 1461);
+        int less = 0;
+        for (int t0 = 0; t0 < nf; t0 += W) {
+            const int i = t0 + l;
+            less += popc(bal(i < nf && key4(i) < K));
+        }
+        need = 24 - less;
     }
-    const int t1 = (k - 1) / 2, t2 = k / 2;
-    const unsigned long long m1 = bal(l < k && rank == t1);
-    const unsigned long long m2 = bal(l < k && rank == t2);
-    const double a = __shfl(v, __ffsll((long long)m1) - 1);
-    const double b = __shfl(v, __ffsll((long long)m2) - 1);
-    return (k & 1) ? a : (a + b) / 2.0;
+    int taken_eq = 0, nsel = 0;
+    for (int t0 = 0; t0 < nf; t0 += W) {
+        const int i = t0 + l;
+        int kv = 1 << 21;
+        if (i < nf) kv = key4(i);
+        const unsigned long long eq = bal(i < nf && kv == K);
+        const bool sel = i < nf && (kv < K || (kv == K && taken_eq + below(eq) < need));
+        taken_eq += popc(eq);
+        const unsigned long long sm = bal(sel);
+        if (sel) L->sel[nsel + below(sm)] = fa + i;
+        nsel += popc(sm);
+    }
+    wsync();
+    const int bnd = l & 7, osub = l >> 3;
+    double ss = 0.0;
+    if (bnd < NB)
+        for (int s2 = osub; s2 < nsel; s2 += 8) {
+            const double e = resid_at(P, bnd, L->sel[s2]);
+            ss += e * e;
+        }
+    ss += __shfl_xor(ss, 8);
+    ss += __shfl_xor(ss, 16);
+    ss += __shfl_xor(ss, 32);
+    if (l < NB) L->comp[l] = sqrt(ss) / 4.0;
+    wsync();
+    P.fl += (unsigned long long)nf * 5 * 13 + 24 * 7 * 18 + 7 * 2;
 }
 
 __device__ void lookforward(Px &P, int &wa, int &wb) {
-    const ccdgpu_params &p = P.A->p;
+    const ccdgpu_params &p = c_args.p;
     const int l = lane();
     int a = wa, b = wb;
     int fa = a, fb = b;
@@ -925,8 +1044,6 @@ __device__ void lookforward(Px &P, int &wa, int &wb) {
     double change = 0.0;
     int nc = p.coef_min;
     double fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
-    double comp[NB];
-    double r[NB] = {0, 0, 0, 0, 0, 0, 0};
     int peek_start = b;
     while (b + P.peek < P.m || !have) {
         nc = num_coefs(p, b - a);
@@ -939,8 +1056,8 @@ __device__ void lookforward(Px &P, int &wa, int &wb) {
             fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
             fit_models(P, fa, fb, nc);
             have = true;
-#pragma unroll
-            for (int band = 0; band < NB; ++band) comp[band] = P.L->rmse[band];
+            if (l < NB) LDS().comp[l] = LDS().rmse[l];
+            wsync();
         } else {
             if (model_span >= 1.33 * fit_span) {
                 fa = a;
@@ -948,60 +1065,13 @@ __device__ void lookforward(Px &P, int &wa, int &wb) {
                 fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
                 fit_models(P, fa, fb, nc);
             }
-            // find_closest_doy(period, peek.stop - 1, fit_window, 24) -> comparison rmse
-            const int nf = fb - fa;
-            const int ref = CDR(P, b + k - 1);
-            auto key4 = [&](int i) -> int {
-                const double d = (double)(CDR(P, fa + i) - ref);
-                const double kk = fabs(rint(d / 365.25) * 365.25 - d);
-                return (int)(kk * 4.0 + 0.5);
-            };
-            int K = 1 << 20, need = 0;
-            if (nf > 24) {
-                auto gen = [&](int i, int &v) -> bool { v = key4(i); return true; };
-                K = kth_int(gen, nf, 23, 0, 1461);
-                int less = 0;
-                for (int t0 = 0; t0 < nf; t0 += W) {
-                    const int i = t0 + l;
-                    less += popc(bal(i < nf && key4(i) < K));
-                }
-                need = 24 - less;
-            }
-            double ss[NB] = {0, 0, 0, 0, 0, 0, 0};
-            int taken_eq = 0;
-            for (int t0 = 0; t0 < nf; t0 += W) {
-                const int i = t0 + l;
-                int kv = 1 << 21;
-                if (i < nf) kv = key4(i);
-                const unsigned long long eq = bal(i < nf && kv == K);
-                const bool sel = i < nf && (kv < K || (kv == K && taken_eq + below(eq) < need));
-                taken_eq += popc(eq);
-                if (sel) {
-#pragma unroll
-                    for (int band = 0; band < NB; ++band) {
-                        const double e = resid_at(P, band, fa + i);
-                        ss[band] += e * e;
-                    }
-                }
-            }
-#pragma unroll
-            for (int band = 0; band < NB; ++band) comp[band] = sqrt(wsum(ss[band])) / 4.0;
-            // closest-DOY keys (5 flops) per selection pass, residuals of the 24 chosen obs
-            P.fl += (unsigned long long)nf * 5 * 13 + 24 * 7 * 18 + 7 * 2;
+            closest_doy_comp(P, fa, fb, b + k - 1);
         }
-        double mag = 0.0;
-        if (l < k) {
-#pragma unroll
-            for (int band = 0; band < NB; ++band) r[band] = resid_at(P, band, b + l);
-            mag = magnitude(P, r, comp);
-        }
-        P.fl += (unsigned long long)k * (7 * 16 + 5 * 4);
-        const bool chg = bal(l < k && !(mag > P.chg)) == 0ull;
-        if (chg) {
+        double m0;
+        if (eval_peek(P, k, b, 1, m0)) {
             change = 1.0;
             break;
         }
-        const double m0 = __shfl(mag, 0);
         if (m0 > p.outlier_threshold) {
             const int rm = b;
             compact_drop(P, rm, [&](int j) { return j == rm; });
@@ -1009,20 +1079,14 @@ __device__ void lookforward(Px &P, int &wa, int &wb) {
         }
         b += 1;
     }
-    // magnitudes: median over the last peek residuals, per band (lane b gets band b)
-    double mag_lane = 0.0;
-#pragma unroll
-    for (int band = 0; band < NB; ++band) {
-        const double md = lane_median(r[band], P.peek);
-        if (l == band) mag_lane = md;
-    }
+    const double mag_lane = peek_medians(P, P.peek);
     emit(P, CDR(P, a), CDR(P, b - 1), CDR(P, peek_start), b - a, change, nc, mag_lane);
     wa = a;
     wb = b;
 }
 
 __device__ void standard_procedure(Px &P) {
-    const ccdgpu_params &p = P.A->p;
+    const ccdgpu_params &p = c_args.p;
     const int meow = p.meow_size;
     variogram(P);
     adjust_peek(P);
@@ -1050,9 +1114,9 @@ __device__ void standard_procedure(Px &P) {
 // ------------------------------------------------------------------ qa.py filters + compaction
 // Returns the procedure, or -1 for an unsupported QA value.
 __device__ int px_setup(Px &P, int chip, int pix) {
-    const CcdDetectArgs &A = *P.A;
+    const CcdDetectArgs &A = c_args;
     const ccdgpu_params &p = A.p;
-    Lds *L = P.L;
+    Lds *L = &LDS();
     const int l = lane();
     const int n = P.n;
     const int32_t *order = A.order + (size_t)chip * n;
@@ -1150,14 +1214,12 @@ __device__ int px_setup(Px &P, int chip, int pix) {
     return proc;
 }
 
-__global__ __launch_bounds__(64) void ccd_detect(const CcdDetectArgs *__restrict__ Ap) {
-    __shared__ Lds lds;
-    const CcdDetectArgs &A = *Ap;
+__device__ __forceinline__ void detect_body() {
+    const CcdDetectArgs &A = c_args;
+    Lds &lds = LDS();
     const int l = lane();
     const int slot = blockIdx.x;
     Px P;
-    P.A = &A;
-    P.L = &lds;
     P.n = A.n_obs;
     P.cd = A.s_date + (size_t)slot * A.n_obs;
     P.ci = A.s_idx + (size_t)slot * A.n_obs;
@@ -1165,6 +1227,7 @@ __global__ __launch_bounds__(64) void ccd_detect(const CcdDetectArgs *__restrict
     P.fs = A.s_f64 + (size_t)slot * 5 * A.n_obs;
     P.fits = 0;
     P.sweeps = 0;
+    P.bad = 0;
     P.fl = 0;
     P.fl_lane = 0;
     for (;;) {
@@ -1203,6 +1266,15 @@ __global__ __launch_bounds__(64) void ccd_detect(const CcdDetectArgs *__restrict
         }
         wsync();
     }
+    // index-guard report (first tripped line of any lane)
+    {
+        int bl = P.bad;
+        for (int o = 32; o > 0; o >>= 1) {
+            const int t = __shfl_xor(bl, o);
+            bl = t > bl ? t : bl;
+        }
+        if (l == 0 && bl) atomicCAS(&A.counters[4], 0ull, (unsigned long long)bl);
+    }
     // instrumentation
     unsigned long long sw = P.sweeps, fll = P.fl_lane;
     for (int o = 32; o > 0; o >>= 1) {
@@ -1215,6 +1287,11 @@ __global__ __launch_bounds__(64) void ccd_detect(const CcdDetectArgs *__restrict
         atomicAdd(&A.stats[2], P.fl + fll);
     }
 }
+
+// Two register budgets of the same body: occupancy-1 (no spills) and 4 waves/SIMD (128 VGPRs,
+// the compiler spills the rest).  The host picks one (CCDGPU_KERNEL=w1|w4; default w4).
+__global__ __launch_bounds__(64) void ccd_detect() { detect_body(); }
+__global__ __launch_bounds__(64, 4) void ccd_detect_w4() { detect_body(); }
 
 // ------------------------------------------------------------------ per-chip preparation
 // One 256-thread block per chip: stable rank of each date (ties by input position), sorted
@@ -1280,8 +1357,16 @@ extern "C" int ccdk_prep(const int64_t *dates, int32_t n_chips, int32_t n_obs, d
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-extern "C" int ccdk_detect(const CcdDetectArgs *dev_args, int32_t grid, void *stream) {
-    hipLaunchKernelGGL(ccd_detect, dim3(grid), dim3(64), 0, (hipStream_t)stream, dev_args);
+extern "C" int ccdk_set_args(const CcdDetectArgs *host_args, void *stream) {
+    return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_args), host_args, sizeof(CcdDetectArgs), 0,
+                                  hipMemcpyHostToDevice, (hipStream_t)stream) == hipSuccess ? 0 : -1;
+}
+
+extern "C" int ccdk_detect(int32_t grid, int variant, void *stream) {
+    if (variant == 1)
+        hipLaunchKernelGGL(ccd_detect, dim3(grid), dim3(64), sizeof(Lds), (hipStream_t)stream);
+    else
+        hipLaunchKernelGGL(ccd_detect_w4, dim3(grid), dim3(64), sizeof(Lds), (hipStream_t)stream);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -80,6 +81,7 @@ struct ccdgpu_ctx {
     int device = 0;
     int n_cu = 0;
     int slots_per_cu = 0;
+    int variant = 4;  // detection kernel register budget: 1 or 4 waves/SIMD (CCDGPU_KERNEL)
     hipStream_t stream = nullptr;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // staged batch
@@ -211,6 +213,8 @@ int ccdgpu_init(int device, ccdgpu_ctx **out) {
     }
     for (auto &e : c->ev) (void)hipEventCreate(&e);
     c->slots_per_cu = 16;
+    if (const char *v = std::getenv("CCDGPU_KERNEL")) c->variant = (std::strcmp(v, "w1") == 0) ? 1 : 4;
+    if (const char *v = std::getenv("CCDGPU_SLOTS_PER_CU")) c->slots_per_cu = std::max(1, std::atoi(v));
     *out = c;
     return 0;
 }
@@ -326,12 +330,12 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         unsigned long long init[8] = {0ull, 0ull, ~0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
         HIPCHK(hipMemcpyAsync(c->counters.p, init, sizeof(init), hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipMemsetAsync(c->stats.p, 0, sizeof(unsigned long long) * 8, c->stream));
-        HIPCHK(hipMemcpyAsync(c->args.p, &a, sizeof(a), hipMemcpyHostToDevice, c->stream));
+        if (ccdk_set_args(&a, c->stream)) return fail(CCDGPU_EHIP, "copying kernel arguments to constant memory failed");
         HIPCHK(hipEventRecord(c->ev[0], c->stream));
         if (ccdk_prep(c->dates.p, c->n_chips, c->n_obs, p.avg_days_yr, c->order.p, c->sdates.p, c->basis.p, c->stream))
             return fail(CCDGPU_EHIP, std::string("prep launch: ") + hipGetErrorString(hipGetLastError()));
         HIPCHK(hipEventRecord(c->ev[1], c->stream));
-        if (ccdk_detect(c->args.p, c->n_slots, c->stream))
+        if (ccdk_detect(c->n_slots, c->variant, c->stream))
             return fail(CCDGPU_EHIP, std::string("detect launch: ") + hipGetErrorString(hipGetLastError()));
         HIPCHK(hipEventRecord(c->ev[2], c->stream));
         unsigned long long h[8];
