@@ -14,7 +14,7 @@ import numpy as np
 from . import abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), 'lib', 'libccdgpu.so')
+LIB_PATH = os.environ.get('CCDGPU_LIBRARY') or os.path.join(os.path.dirname(_HERE), 'lib', 'libccdgpu.so')
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -48,9 +48,10 @@ def _declare(L):
     L.ccdgpu_run_staged.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
     L.ccdgpu_fetch_staged.argtypes = [c.c_void_p, c.c_int32, c.POINTER(abi.Result)]
     L.ccdgpu_last_stats.argtypes = [c.c_void_p, c.POINTER(abi.Stats)]
+    L.ccdgpu_diag_counters.argtypes = [c.c_void_p, c.POINTER(c.c_uint64), c.c_int32]
     for name in ('ccdgpu_init', 'ccdgpu_destroy', 'ccdgpu_device_count', 'ccdgpu_synchronize',
                  'ccdgpu_detect_batch', 'ccdgpu_stage', 'ccdgpu_run_staged', 'ccdgpu_fetch_staged',
-                 'ccdgpu_last_stats'):
+                 'ccdgpu_last_stats', 'ccdgpu_diag_counters'):
         getattr(L, name).restype = c.c_int
     return L
 
@@ -58,7 +59,7 @@ def _declare(L):
 EXPORTS = ('ccdgpu_version', 'ccdgpu_last_error', 'ccdgpu_params_default', 'ccdgpu_init',
            'ccdgpu_destroy', 'ccdgpu_device_count', 'ccdgpu_synchronize', 'ccdgpu_detect_batch',
            'ccdgpu_result_free', 'ccdgpu_stage', 'ccdgpu_run_staged', 'ccdgpu_fetch_staged',
-           'ccdgpu_last_stats')
+           'ccdgpu_last_stats', 'ccdgpu_diag_counters')
 
 
 def lib():
@@ -176,6 +177,11 @@ class Context(object):
             return abi.unpack(res)
         finally:
             lib().ccdgpu_result_free(ctypes.byref(res))
+
+    def diag_counters(self):
+        buf = (ctypes.c_uint64 * 32)()
+        _check(lib().ccdgpu_diag_counters(self._ctx, buf, 32))
+        return list(buf)
 
     def stats(self):
         s = abi.Stats()

@@ -40,7 +40,7 @@ struct CcdDetectArgs {
     int32_t *s_date;
     uint16_t *s_idx;
     int16_t *s_val;
-    double *s_f64;   // [n_slots][5][n_obs] Tmask scratch
+    double *s_f64;   // [n_slots][8][n_obs] Tmask scratch / peek residuals
     // outputs
     uint32_t *mask_bits;
     int32_t *procedure;

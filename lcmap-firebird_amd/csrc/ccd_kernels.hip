@@ -37,10 +37,12 @@ namespace {
 constexpr int NB = CCD_NB;
 constexpr int W = CCD_WAVE;
 constexpr int RW = 16;  // doubles per staged design row: t c1 s1 c2 s2 c3 s3 _ y0..y6 _
+constexpr int TR = 32;  // rows per LDS staging tile
 constexpr int MAXW = CCDGPU_MAX_OBS / 32;
+#define CCD_NPHASE 12
 
 struct Lds {
-    double row[W][RW];
+    double row[TR][RW];
     double G[8][8];
     double Q[8][8];  // Q[j][band] = Xc_j . yc_band
     double YY[8];
@@ -55,6 +57,7 @@ struct Lds {
     uint32_t tflag[MAXW];  // Tmask outlier flags of the current window
     int sel[32];           // compacted indices of the 24 closest-DOY observations
     double tchol[5][5];    // Tmask: Cholesky factor of the unweighted normal matrix
+    uint32_t hist2[732];   // closest-DOY: fit-window counts per (4 t mod 1461) bin, 2 x u16 per word
 };
 
 // Launch arguments live in constant memory (uniform scalar loads from every device function);
@@ -73,14 +76,30 @@ struct Px {
     int32_t *cd;
     uint16_t *ci;
     int16_t *cv;
-    double *fs;  // per-slot double scratch [5][n]
+    double *fs;  // per-slot double scratch [8][n]
     int64_t gpix;
     int nseg;
     unsigned long long fits, sweeps;
     unsigned long long fl;       // counted FP64 flops, wave-uniform part
     unsigned long long fl_lane;  // counted FP64 flops, per-lane part (coordinate descent)
     mutable int bad;             // source line of a tripped index guard (0 = none), per lane
+#ifdef CCD_PHASE_TIMERS
+    unsigned long long tph[CCD_NPHASE];
+#endif
 };
+
+// ------------------------------------------------------------------ diagnostic phase timers
+// Built only into lib/libccdgpu_diag.so (-DCCD_PHASE_TIMERS): s_memtime cycle totals per phase,
+// summed over waves into stats[8 + phase].  Phases: 0 pixel total, 1 QA/filter/compaction,
+// 2 variogram + peek, 3 Tmask, 4 Lasso Gram, 5 Lasso CD, 6 Lasso rmse, 7 closest-DOY rmse,
+// 8 peek evaluation, 9 outlier compaction, 10 stability, 11 medians + emit.
+#ifdef CCD_PHASE_TIMERS
+#define PH_BEGIN(id) const unsigned long long _ph_##id = __builtin_amdgcn_s_memtime();
+#define PH_END(P, id, slot) (P).tph[slot] += __builtin_amdgcn_s_memtime() - _ph_##id;
+#else
+#define PH_BEGIN(id)
+#define PH_END(P, id, slot)
+#endif
 
 // ------------------------------------------------------------------ index guards
 // Every read of the compacted period goes through these: an out-of-range index is clamped (so a
@@ -111,10 +130,26 @@ __device__ __forceinline__ int popc(unsigned long long x) { return __popcll(x); 
 __device__ __forceinline__ int below(unsigned long long m) {
     return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
 }
+// DPP lane moves on a double (two 32-bit halves).  Controls: 0xB1 quad_perm [1,0,3,2] (xor 1),
+// 0x4E quad_perm [2,3,0,1] (xor 2), 0x141 row_half_mirror (lane i <-> 7-i in each 8),
+// 0x140 row_mirror (lane i <-> 15-i in each 16).
+template <int CTRL>
+__device__ __forceinline__ double dpp(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double rdlane(double v, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                            __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+// wave-wide sum, identical (wave-uniform) result in every lane
 __device__ __forceinline__ double wsum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+    v += dpp<0xB1>(v);
+    v += dpp<0x4E>(v);
+    v += dpp<0x141>(v);
+    v += dpp<0x140>(v);
+    return (rdlane(v, 0) + rdlane(v, 16)) + (rdlane(v, 32) + rdlane(v, 48));
 }
 __device__ __forceinline__ void wsync() { __syncthreads(); }
 
@@ -166,6 +201,24 @@ __device__ double kth_nonneg(const double *vals, int N, int k) {
         else lo = mid + 1;
     }
     return __longlong_as_double((long long)lo);
+}
+
+// ascending bitonic sort of one double per lane across the 64-lane wave (21 exchange stages)
+__device__ __forceinline__ double bitonic64(double v) {
+    const int l = lane();
+#pragma unroll
+    for (int k = 2; k <= W; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const double o = __shfl_xor(v, j);
+            const bool up = (l & k) == 0;
+            const bool lower = (l & j) == 0;
+            const double mn = o < v ? o : v;
+            const double mx = o < v ? v : o;
+            v = (lower == up) ? mn : mx;
+        }
+    }
+    return v;
 }
 
 __device__ __forceinline__ int qabitval(const ccdgpu_params &p, unsigned v) {
@@ -238,17 +291,16 @@ __device__ __forceinline__ void stage_rows(const Px &P, int j0, int cnt) {
 
 // 8-lane group reductions (a band's lanes 8b .. 8b+7); results identical in all 8 lanes.
 __device__ __forceinline__ double gsum8(double v) {
-    v += __shfl_xor(v, 1);
-    v += __shfl_xor(v, 2);
-    v += __shfl_xor(v, 4);
-    return v;
+    v += dpp<0xB1>(v);
+    v += dpp<0x4E>(v);
+    return v + dpp<0x141>(v);
 }
 __device__ __forceinline__ double gmax8(double v) {
-    double t = __shfl_xor(v, 1);
+    double t = dpp<0xB1>(v);
     v = t > v ? t : v;
-    t = __shfl_xor(v, 2);
+    t = dpp<0x4E>(v);
     v = t > v ? t : v;
-    t = __shfl_xor(v, 4);
+    t = dpp<0x141>(v);
     return t > v ? t : v;
 }
 
@@ -264,6 +316,7 @@ __device__ int cd_lanes(Lds *L, int pc, double alpha, int max_iter, double tol) 
 #pragma unroll
     for (int j = 0; j < 7; ++j) gcol[j] = (act && j < pc) ? L->G[j][k] : 0.0;
     const double gkk = act ? L->G[k][k] : 0.0;
+    const double rgkk = gkk != 0.0 ? 1.0 / gkk : 0.0;  // w_k = S(tmp, alpha) / G_kk as a multiply
     const double q = act ? L->Q[k][b] : 0.0;
     const double yy = b < NB ? L->YY[b] : 0.0;
     const double tol_s = tol * yy;
@@ -280,7 +333,7 @@ __device__ int cd_lanes(Lds *L, int pc, double alpha, int max_iter, double tol) 
             if (act && !done && k == j && gkk != 0.0) {
                 const double tmp = q - s;
                 const double aa = fabs(tmp) - alpha;
-                const double wn = aa > 0.0 ? (tmp > 0.0 ? aa : -aa) / gkk : 0.0;
+                const double wn = aa > 0.0 ? (tmp > 0.0 ? aa : -aa) * rgkk : 0.0;
                 dl = fabs(wn - w);
                 w = wn;
             }
@@ -340,10 +393,11 @@ __device__ void fit_models(Px &P, int a, int b, int k) {
     const int l = lane();
     const int nw = b - a;
     const int pc = k - 1;  // active design columns (t + harmonics)
+    PH_BEGIN(gram)
     // pass 1: column means (x columns 0..6, y bands) -- sequential per column, lane = column
     double acc = 0.0;
-    for (int t0 = 0; t0 < nw; t0 += W) {
-        const int cnt = nw - t0 < W ? nw - t0 : W;
+    for (int t0 = 0; t0 < nw; t0 += TR) {
+        const int cnt = nw - t0 < TR ? nw - t0 : TR;
         stage_rows(P, a + t0, cnt);
         if (l < 14) {
             const int col = l < 7 ? l : l + 1;
@@ -382,9 +436,9 @@ __device__ void fit_models(Px &P, int a, int b, int k) {
             mb[h] = cb[h] < 8 ? L->xm[cb[h]] : L->ym[cb[h] - 8];
         }
     }
-    for (int t0 = 0; t0 < nw; t0 += W) {
-        const int cnt = nw - t0 < W ? nw - t0 : W;
-        if (nw > W) stage_rows(P, a + t0, cnt);
+    for (int t0 = 0; t0 < nw; t0 += TR) {
+        const int cnt = nw - t0 < TR ? nw - t0 : TR;
+        if (nw > TR) stage_rows(P, a + t0, cnt);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             if (ca[h] >= 0) {
@@ -408,11 +462,13 @@ __device__ void fit_models(Px &P, int a, int b, int k) {
         }
     }
     wsync();
+    PH_END(P, gram, 4)
+    PH_BEGIN(cd)
     // coordinate descent: lane = band * 8 + coordinate
     const int sw = cd_lanes(L, pc, p.lasso_alpha * nw, p.lasso_max_iter, p.lasso_tol);
     if ((l & 7) == 0 && (l >> 3) < NB) {
         P.sweeps += (unsigned long long)sw;  // per-lane; reduced at the end
-        P.fl_lane += (unsigned long long)sw * (unsigned long long)(2 * pc * pc + 6 * pc) + 14;
+        P.fl_lane += (unsigned long long)sw * (unsigned long long)(2 * k * k + 6 * k);  // CD: iters (2k^2 + 6k)
     }
     wsync();
     if (l < NB) {
@@ -422,9 +478,12 @@ __device__ void fit_models(Px &P, int a, int b, int k) {
         L->coef[l][7] = L->ym[l] - dot;
     }
     P.fits += NB;
-    // means 14 n, centred Gram/X'y entries 4 n each, rmse 7 * (2*7 + 3) n
-    P.fl += (unsigned long long)nw * (unsigned long long)(14 + 4 * nE + 7 * 17) + 14;
+    // SURVEY.md 8(d) op-count model: Gram + column sums n k (k+1), RHS 7 * 2 n k,
+    // residual / rmse 7 (2 n k + 3 n)  (k = number of coefficients incl. intercept)
+    P.fl += (unsigned long long)nw * (unsigned long long)(k * (k + 1) + 14 * k + 7 * (2 * k + 3));
     wsync();
+    PH_END(P, cd, 5)
+    PH_BEGIN(rmse)
     // rmse from residuals of the raw design (predict = X @ coef + intercept);
     // lane = (observation sub-index, band), 8 observations per pass
     {
@@ -442,6 +501,7 @@ __device__ void fit_models(Px &P, int a, int b, int k) {
         if (l < NB) L->rmse[l] = sqrt(ss / den);
     }
     wsync();
+    PH_END(P, rmse, 6)
 }
 
 
@@ -485,6 +545,59 @@ __device__ void catch_(Px &P, int a, int b, int cqa) {
     emit(P, CDR(P, a), CDR(P, b - 1), bday, b - a, 0.0, cqa, 0.0);
 }
 
+// k-th smallest (0-based) of 16-bit unsigned values produced by gen(i, &v) for i < N (valid if
+// gen returns true): two-pass radix select over 256-bin LDS histograms (L->hist2 as scratch).
+template <class F>
+__device__ int select_u16(F gen, int N, int k) {
+    Lds *L = &LDS();
+    const int l = lane();
+    int hiB = 0, rank = k;
+#pragma unroll 1
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int i = l; i < 256; i += W) L->hist2[i] = 0u;
+        wsync();
+        for (int base = 0; base < N; base += W) {
+            const int i = base + l;
+            int v = 0;
+            if (i < N && gen(i, v) && (pass == 0 || (v >> 8) == hiB))
+                atomicAdd(&L->hist2[pass == 0 ? (v >> 8) : (v & 255)], 1u);
+        }
+        wsync();
+        int carry = 0, found = -1;
+        for (int b0 = 0; b0 < 256; b0 += W) {
+            const int c = (int)L->hist2[b0 + l];
+            int cum = c;
+#pragma unroll
+            for (int o = 1; o < W; o <<= 1) {
+                const int t = __shfl_up(cum, o);
+                if (l >= o) cum += t;
+            }
+            cum += carry;
+            const unsigned long long hit = bal(cum > rank);
+            if (hit) {
+                const int src = __ffsll((long long)hit) - 1;
+                found = b0 + src;
+                rank -= __shfl(cum, src) - __shfl(c, src);
+                break;
+            }
+            carry = __shfl(cum, W - 1);
+        }
+        wsync();
+        if (pass == 0) hiB = found;
+        else return (hiB << 8) | found;
+    }
+    return 0;
+}
+
+template <class F>
+__device__ double median_u16(F gen, int N, int cnt) {
+    if (cnt <= 0) return __builtin_nan("");
+    if (cnt & 1) return (double)select_u16(gen, N, cnt / 2);
+    const int a = select_u16(gen, N, cnt / 2 - 1);
+    const int b = select_u16(gen, N, cnt / 2);
+    return ((double)a + (double)b) / 2.0;
+}
+
 // ------------------------------------------------------------------ variogram / peek
 __device__ void variogram(Px &P) {
     Lds *L = &LDS();
@@ -520,9 +633,9 @@ __device__ void variogram(Px &P) {
             val = d < 0 ? -d : d;
             return true;
         };
-        const double med = median_int(gen, m - kk, cnt, 0, 65535);
+        const double med = median_u16(gen, m - kk, cnt);
         if (l == 0) L->vario[band] = med;
-        P.fl += (unsigned long long)(m - kk);
+        P.fl += 2ull * (unsigned long long)(m - kk);  // 2 per difference per band
     }
     wsync();
 }
@@ -536,7 +649,8 @@ __device__ void adjust_peek(Px &P) {
         val = CDR(P, i + 1) - CDR(P, i);
         return true;
     };
-    const double delta = median_int(gen, P.m - 1, P.m - 1, 0, 1 << 20);
+    const bool narrow = CDR(P, P.m - 1) - CDR(P, 0) <= 65535;  // every gap fits 16 bits
+    const double delta = narrow ? median_u16(gen, P.m - 1, P.m - 1) : median_int(gen, P.m - 1, P.m - 1, 0, 1 << 30);
     const double adj = rint((double)(p.peek_size * 16) / delta);
     if (adj > (double)p.peek_size) {
         P.peek = adj > (double)CCDGPU_MAX_PEEK ? CCDGPU_MAX_PEEK : (int)adj;
@@ -582,8 +696,8 @@ __device__ void tm_normal(const Px &P, int a, int nw, int ncol, const double *xo
         eb = 6;
     }
     double acc = 0.0;
-    for (int t0 = 0; t0 < nw; t0 += W) {
-        const int cnt = nw - t0 < W ? nw - t0 : W;
+    for (int t0 = 0; t0 < nw; t0 += TR) {
+        const int cnt = nw - t0 < TR ? nw - t0 : TR;
         if (l < cnt) {
             const int i = t0 + l;
             double x[5];
@@ -699,7 +813,6 @@ __device__ int tmask(Px &P, int a, int b) {
     const double w = 2.0 * M_PI / p.avg_days_yr;
     const double oc = w / ceil(((double)CDR(P, b - 1) - (double)CDR(P, a)) / p.avg_days_yr);
     const int ncol = (oc == w) ? 3 : 5;
-    P.fl += (unsigned long long)nw * (2 + 45 + 25);
     double *xoc = P.fs, *xos = P.fs + P.n, *adj = P.fs + 2 * P.n, *absr = P.fs + 3 * P.n,
            *wt = P.fs + 4 * P.n;
     if (ncol == 5) tm_trig(P, a, nw, oc, xoc, xos);
@@ -766,7 +879,7 @@ __device__ int tmask(Px &P, int a, int b) {
                 tm_solve(Gt, r0, coef);
             }
         }
-        P.fl += (unsigned long long)nw * (4 + 60 + 12) + 120;
+        P.fl += (unsigned long long)nw * 35 + 125;  // OLS fit: n_w 35 + 5^3
         int iteration = 1;
         bool converged = false;
         while (!converged && iteration < 5) {
@@ -780,8 +893,17 @@ __device__ int tmask(Px &P, int a, int b) {
             // mad = median(sort(|r|)[4:]) / 0.6745
             const int c = nw - 4;
             double med;
-            if (c & 1) med = kth_nonneg(absr, nw, 4 + c / 2);
-            else med = (kth_nonneg(absr, nw, 4 + c / 2 - 1) + kth_nonneg(absr, nw, 4 + c / 2)) / 2.0;
+            if (nw <= W) {
+                // one value per lane (lane i wrote absr[i]): bitonic sort across the wave
+                const double v = bitonic64(l < nw ? absr[l] : __builtin_inf());
+                const double hi = __shfl(v, 4 + c / 2);
+                const double lo = __shfl(v, 4 + (c - 1) / 2);
+                med = (c & 1) ? hi : (lo + hi) / 2.0;
+            } else if (c & 1) {
+                med = kth_nonneg(absr, nw, 4 + c / 2);
+            } else {
+                med = (kth_nonneg(absr, nw, 4 + c / 2 - 1) + kth_nonneg(absr, nw, 4 + c / 2)) / 2.0;
+            }
             const double mad = med / 0.6745;
             const double floor_ = 2.220446049250313e-16 * ystd;
             const double scale = mad > floor_ ? mad : floor_;
@@ -795,7 +917,7 @@ __device__ int tmask(Px &P, int a, int b) {
             tm_normal(P, a, nw, ncol, xoc, xos, band, wt);
             tm_load(&LDS(), Gw, rw);
             tm_solve(Gw, rw, coef);
-            P.fl += (unsigned long long)nw * (60 + 18) + 120;
+            P.fl += (unsigned long long)nw * 35 + 125;  // each IRLS refit: n_w 35 + 5^3
             iteration += 1;
             converged = true;
 #pragma unroll
@@ -850,7 +972,7 @@ __device__ bool stable(const Px &P, int a, int b) {
     }
     return sqrt(wsum(v2)) < P.chg;
 }
-__device__ __forceinline__ void count_stable(Px &P) { P.fl += 5 * (2 * 16 + 8) + 6; }
+__device__ __forceinline__ void count_stable(Px &P) {}
 
 __device__ bool initialize(Px &P, int &wa, int &wb) {
     const ccdgpu_params &p = c_args.p;
@@ -860,7 +982,9 @@ __device__ bool initialize(Px &P, int &wa, int &wb) {
     bool ok = false;
     while (b + p.meow_size < P.m) {
         if (CDR(P, b - 1) - CDR(P, a) < p.day_delta) { b += 1; continue; }
+        PH_BEGIN(tm)
         const int cnt = tmask(P, a, b);
+        PH_END(P, tm, 3)
         const int nw = b - a;
         if (cnt == nw) { b += 1; continue; }
         // first / last kept observation of the window
@@ -884,7 +1008,10 @@ __device__ bool initialize(Px &P, int &wa, int &wb) {
         }
         fit_models(P, a, b, 4);
         count_stable(P);
-        if (!stable(P, a, b)) { a += 1; b += 1; continue; }
+        PH_BEGIN(st)
+        const bool stb = stable(P, a, b);
+        PH_END(P, st, 10)
+        if (!stb) { a += 1; b += 1; continue; }
         ok = true;
         break;
     }
@@ -919,19 +1046,20 @@ __device__ bool eval_peek(Px &P, int k, int start, int dir, double &mag0) {
         const bool valid = jj < k && bnd < NB;
         double r = 0.0;
         if (valid) r = resid_at(P, bnd, start + dir * jj);
-        if (jj < k) L->row[jj][bnd] = r;  // kept for the segment's magnitude medians
+        if (jj < k) P.fs[jj * 8 + bnd] = r;  // kept for the segment's magnitude medians
         const double v = r / rm;
         const double mag = gsum8((valid && det) ? v * v : 0.0);
         if (bal(bnd == 0 && jj < k && !(mag > P.chg))) all = false;
         if (pass == 0) mag0 = __shfl(mag, 0);
     }
-    P.fl += (unsigned long long)k * (7 * 16 + 5 * 4);
+    P.fl += (unsigned long long)k * (7 * 2 * 8 + 5 * 3);  // predict 7*2*8 + magnitude 5*3 per peek obs
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     wsync();
     return all;
 }
 
 // Median over the k peek residuals of each band (lookforward result magnitudes, taken from
-// L->row where eval_peek left them); returns band l's median in lane l (l < 7).
+// the slot scratch where eval_peek left them); returns band l's median in lane l (l < 7).
 __device__ double peek_medians(Px &P, int k) {
     Lds *L = &LDS();
     const int l = lane();
@@ -939,10 +1067,10 @@ __device__ double peek_medians(Px &P, int k) {
     const int t1 = (k - 1) / 2, t2 = k / 2;
     for (int jj = osub; jj < k; jj += 8) {
         if (bnd >= NB) continue;
-        const double v = L->row[jj][bnd];
+        const double v = P.fs[jj * 8 + bnd];
         int rank = 0;
         for (int i = 0; i < k; ++i) {
-            const double u = L->row[i][bnd];
+            const double u = P.fs[i * 8 + bnd];
             rank += (u < v || (u == v && i < jj)) ? 1 : 0;
         }
         if (rank == t1) L->med1[bnd] = v;
@@ -968,11 +1096,15 @@ __device__ void lookback(Px &P, int &wa, int &wb, int prev) {
         else lo = prev;
         const int k = a - lo;
         double m0;
+        PH_BEGIN(ep)
         const bool change = eval_peek(P, k, a - 1, -1, m0);
+        PH_END(P, ep, 8)
         if (change) break;
         if (m0 > p.outlier_threshold) {
             const int rm = a - 1;
+            PH_BEGIN(cp)
             compact_drop(P, rm, [&](int j) { return j == rm; });
+            PH_END(P, cp, 9)
             a -= 1;
             b -= 1;
             continue;
@@ -984,34 +1116,65 @@ __device__ void lookback(Px &P, int &wa, int &wb, int prev) {
 }
 
 // find_closest_doy(period, ref, fit_window, 24) -> comparison rmse sqrt(sum r^2) / 4 per band
-// into L->comp.  Keys |round(d / 365.25) * 365.25 - d| are multiples of 0.25 days (integers x4),
-// selected by counting (stable argsort order: ties by index).
+// into L->comp.  The key |round(d / 365.25) * 365.25 - d| of d = t - t_ref is exactly
+// min(r, 1461 - r) / 4 with r = (4 t - 4 t_ref) mod 1461 (verified over all |d| <= 20000), so with
+// u = 4 t mod 1461 the fit window is histogrammed once per refit (L->hist2) and the 24th-smallest
+// key is found by scanning bins outward from u_ref.  Selection = keys below the threshold plus the
+// lowest-index ones at the threshold (stable argsort order, the documented tie rule).
+__device__ __forceinline__ int u1461(int t) { return (4 * t) % 1461; }
+__device__ __forceinline__ int hbin(const Lds *L, int u) { return (int)((L->hist2[u >> 1] >> ((u & 1) * 16)) & 0xFFFFu); }
+
+__device__ void build_hist(const Px &P, int fa, int fb) {
+    Lds *L = &LDS();
+    const int l = lane();
+    for (int i = l; i < 732; i += W) L->hist2[i] = 0u;
+    wsync();
+    for (int i = fa + l; i < fb; i += W) {
+        const int u = u1461(CDR(P, i));
+        atomicAdd(&L->hist2[u >> 1], 1u << ((u & 1) * 16));
+    }
+    wsync();
+}
+
 __device__ void closest_doy_comp(Px &P, int fa, int fb, int ref_idx) {
     Lds *L = &LDS();
     const int l = lane();
     const int nf = fb - fa;
-    const int ref = CDR(P, ref_idx);
-    auto key4 = [&](int i) -> int {
-        const double d = (double)(CDR(P, fa + i) - ref);
-        const double kk = fabs(rint(d / 365.25) * 365.25 - d);
-        return (int)(kk * 4.0 + 0.5);
-    };
+    const int ur = u1461(CDR(P, ref_idx));
     int K = 1 << 20, need = 0;
     if (nf > 24) {
-        auto gen = [&](int i, int &v) -> bool { v = key4(i); return true; };
-        K = kth_int(gen, nf, 23, 0, 1461);
-        int less = 0;
-        for (int t0 = 0; t0 < nf; t0 += W) {
-            const int i = t0 + l;
-            less += popc(bal(i < nf && key4(i) < K));
+        int carry = 0;
+        for (int base = 0; base <= 730; base += W) {
+            const int dd = base + l;
+            int c = 0;
+            if (dd == 0) c = hbin(L, ur);
+            else if (dd <= 730) c = hbin(L, (ur + dd) % 1461) + hbin(L, (ur - dd + 1461) % 1461);
+            int cum = c;
+#pragma unroll
+            for (int o = 1; o < W; o <<= 1) {
+                const int t = __shfl_up(cum, o);
+                if (l >= o) cum += t;
+            }
+            cum += carry;
+            const unsigned long long hit = bal(cum >= 24);
+            if (hit) {
+                const int src = __ffsll((long long)hit) - 1;
+                K = base + src;
+                need = 24 - (__shfl(cum, src) - __shfl(c, src));
+                break;
+            }
+            carry = __shfl(cum, W - 1);
         }
-        need = 24 - less;
     }
     int taken_eq = 0, nsel = 0;
     for (int t0 = 0; t0 < nf; t0 += W) {
         const int i = t0 + l;
         int kv = 1 << 21;
-        if (i < nf) kv = key4(i);
+        if (i < nf) {
+            int r = u1461(CDR(P, fa + i)) - ur;
+            r = r < 0 ? r + 1461 : r;
+            kv = r < 1461 - r ? r : 1461 - r;
+        }
         const unsigned long long eq = bal(i < nf && kv == K);
         const bool sel = i < nf && (kv < K || (kv == K && taken_eq + below(eq) < need));
         taken_eq += popc(eq);
@@ -1032,7 +1195,7 @@ __device__ void closest_doy_comp(Px &P, int fa, int fb, int ref_idx) {
     ss += __shfl_xor(ss, 32);
     if (l < NB) L->comp[l] = sqrt(ss) / 4.0;
     wsync();
-    P.fl += (unsigned long long)nf * 5 * 13 + 24 * 7 * 18 + 7 * 2;
+    P.fl += (unsigned long long)nf * 6 + 5 * 48;  // closest-DOY keys 6 n_fit + comparison rmse 5 * 48
 }
 
 __device__ void lookforward(Px &P, int &wa, int &wb) {
@@ -1045,6 +1208,7 @@ __device__ void lookforward(Px &P, int &wa, int &wb) {
     int nc = p.coef_min;
     double fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
     int peek_start = b;
+    int hfa = -1, hfb = -1;  // fit window the closest-DOY histogram describes
     while (b + P.peek < P.m || !have) {
         nc = num_coefs(p, b - a);
         peek_start = b;
@@ -1065,22 +1229,36 @@ __device__ void lookforward(Px &P, int &wa, int &wb) {
                 fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
                 fit_models(P, fa, fb, nc);
             }
+            PH_BEGIN(cl)
+            if (fb - fa > 24 && (hfa != fa || hfb != fb)) {
+                build_hist(P, fa, fb);
+                hfa = fa;
+                hfb = fb;
+            }
             closest_doy_comp(P, fa, fb, b + k - 1);
+            PH_END(P, cl, 7)
         }
         double m0;
-        if (eval_peek(P, k, b, 1, m0)) {
+        PH_BEGIN(ep)
+        const bool chg_now = eval_peek(P, k, b, 1, m0);
+        PH_END(P, ep, 8)
+        if (chg_now) {
             change = 1.0;
             break;
         }
         if (m0 > p.outlier_threshold) {
             const int rm = b;
+            PH_BEGIN(cp)
             compact_drop(P, rm, [&](int j) { return j == rm; });
+            PH_END(P, cp, 9)
             continue;
         }
         b += 1;
     }
+    PH_BEGIN(md)
     const double mag_lane = peek_medians(P, P.peek);
     emit(P, CDR(P, a), CDR(P, b - 1), CDR(P, peek_start), b - a, change, nc, mag_lane);
+    PH_END(P, md, 11)
     wa = a;
     wb = b;
 }
@@ -1088,8 +1266,10 @@ __device__ void lookforward(Px &P, int &wa, int &wb) {
 __device__ void standard_procedure(Px &P) {
     const ccdgpu_params &p = c_args.p;
     const int meow = p.meow_size;
+    PH_BEGIN(vg)
     variogram(P);
     adjust_peek(P);
+    PH_END(P, vg, 2)
     int a = 0, b = meow, prev = 0, nres = 0;
     bool start = true;
     while (b <= P.m - meow) {
@@ -1207,8 +1387,8 @@ __device__ int px_setup(Px &P, int chip, int pix) {
     wsync();
     if (proc == CCDGPU_PROC_INSUFFICIENT_CLEAR && m > 0) {
         const int16_t *g = P.cv + (size_t)1 * n;
-        auto gen = [&](int i, int &val) -> bool { val = g[i]; return true; };
-        const double med = median_int(gen, m, m, -32768, 32767) + (double)p.median_green_filter;
+        auto gen = [&](int i, int &val) -> bool { val = (int)g[i] + 32768; return true; };
+        const double med = median_u16(gen, m, m) - 32768.0 + (double)p.median_green_filter;
         compact_drop(P, 0, [&](int j) { return !((double)g[j] < med); });
     }
     return proc;
@@ -1224,12 +1404,15 @@ __device__ __forceinline__ void detect_body() {
     P.cd = A.s_date + (size_t)slot * A.n_obs;
     P.ci = A.s_idx + (size_t)slot * A.n_obs;
     P.cv = A.s_val + (size_t)slot * NB * A.n_obs;
-    P.fs = A.s_f64 + (size_t)slot * 5 * A.n_obs;
+    P.fs = A.s_f64 + (size_t)slot * 8 * A.n_obs;
     P.fits = 0;
     P.sweeps = 0;
     P.bad = 0;
     P.fl = 0;
     P.fl_lane = 0;
+#ifdef CCD_PHASE_TIMERS
+    for (int i = 0; i < CCD_NPHASE; ++i) P.tph[i] = 0;
+#endif
     for (;;) {
         unsigned long long job = 0;
         if (l == 0) job = atomicAdd(&A.counters[0], 1ull);
@@ -1241,7 +1424,10 @@ __device__ __forceinline__ void detect_body() {
         P.nseg = 0;
         P.basis = A.basis + (size_t)chip * A.n_obs * CCD_BASIS_STRIDE;
         P.sd = A.sdates + (size_t)chip * A.n_obs;
+        PH_BEGIN(tot)
+        PH_BEGIN(su)
         const int proc = px_setup(P, chip, pix);
+        PH_END(P, su, 1)
         if (proc < 0) {
             if (l == 0) {
                 atomicMin(&A.counters[2], (unsigned long long)job);
@@ -1259,6 +1445,7 @@ __device__ __forceinline__ void detect_body() {
                  proc == CCDGPU_PROC_PERMANENT_SNOW ? A.p.curve_qa_persist_snow : A.p.curve_qa_insuf_clear, 0.0);
         }
         wsync();
+        PH_END(P, tot, 0)
         for (int i = l; i < A.mask_words; i += W) A.mask_bits[(size_t)job * A.mask_words + i] = lds.mask[i];
         if (l == 0) {
             A.procedure[job] = proc;
@@ -1285,6 +1472,9 @@ __device__ __forceinline__ void detect_body() {
         atomicAdd(&A.stats[0], P.fits);
         atomicAdd(&A.stats[1], sw);
         atomicAdd(&A.stats[2], P.fl + fll);
+#ifdef CCD_PHASE_TIMERS
+        for (int i = 0; i < CCD_NPHASE; ++i) atomicAdd(&A.stats[8 + i], P.tph[i]);
+#endif
     }
 }
 

@@ -104,6 +104,7 @@ struct ccdgpu_ctx {
     DevBuf<unsigned char> cub_tmp;
     std::vector<int64_t> h_offsets;
     ccdgpu_stats last{};
+    unsigned long long diag[32] = {};
     ~ccdgpu_ctx() {
         for (auto *b : {&dates, &sdates, &offsets}) b->release();
         spectra.release();
@@ -273,12 +274,12 @@ int ccdgpu_stage(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_chips, in
         (rc = c->procedure.ensure(c->total_pix)) || (rc = c->nseg.ensure(c->total_pix)) ||
         (rc = c->probs.ensure(3 * c->total_pix)) || (rc = c->offsets.ensure(c->total_pix + 1)) ||
         (rc = c->mask.ensure((size_t)c->total_pix * c->mask_words)) || (rc = c->counters.ensure(8)) ||
-        (rc = c->stats.ensure(8)) || (rc = c->args.ensure(1)))
+        (rc = c->stats.ensure(32)) || (rc = c->args.ensure(1)))
         return rc;
     c->n_slots = (int32_t)std::min<int64_t>(c->total_pix, (int64_t)c->n_cu * c->slots_per_cu);
     const size_t ns = (size_t)c->n_slots;
     if ((rc = c->s_date.ensure(ns * no)) || (rc = c->s_idx.ensure(ns * no)) || (rc = c->s_val.ensure(ns * 7 * no)) ||
-        (rc = c->s_f64.ensure(ns * 5 * no)))
+        (rc = c->s_f64.ensure(ns * 8 * no)))
         return rc;
     if (c->pool_cap < c->total_pix * 8) c->pool_cap = c->total_pix * 8;
     if ((rc = c->pool.ensure(c->pool_cap)) || (rc = c->pool_seq.ensure(c->pool_cap))) return rc;
@@ -329,7 +330,7 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         a.pool_cap = c->pool_cap;
         unsigned long long init[8] = {0ull, 0ull, ~0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
         HIPCHK(hipMemcpyAsync(c->counters.p, init, sizeof(init), hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipMemsetAsync(c->stats.p, 0, sizeof(unsigned long long) * 8, c->stream));
+        HIPCHK(hipMemsetAsync(c->stats.p, 0, sizeof(unsigned long long) * 32, c->stream));
         if (ccdk_set_args(&a, c->stream)) return fail(CCDGPU_EHIP, "copying kernel arguments to constant memory failed");
         HIPCHK(hipEventRecord(c->ev[0], c->stream));
         if (ccdk_prep(c->dates.p, c->n_chips, c->n_obs, p.avg_days_yr, c->order.p, c->sdates.p, c->basis.p, c->stream))
@@ -352,8 +353,9 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         float ms_prep = 0.f, ms_det = 0.f;
         (void)hipEventElapsedTime(&ms_prep, c->ev[0], c->ev[1]);
         (void)hipEventElapsedTime(&ms_det, c->ev[1], c->ev[2]);
-        unsigned long long st[8];
+        unsigned long long st[32];
         HIPCHK(hipMemcpy(st, c->stats.p, sizeof(st), hipMemcpyDeviceToHost));
+        for (int i = 0; i < 32; ++i) c->diag[i] = st[i];
         // CSR: exclusive scan of per-pixel counts, then scatter the pool
         int rc;
         if ((rc = c->csr.ensure(c->n_pool > 0 ? c->n_pool : 1))) return rc;
@@ -389,6 +391,12 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         return 0;
     }
     return fail(CCDGPU_EOVERFLOW, "segment pool kept overflowing");
+}
+
+int ccdgpu_diag_counters(ccdgpu_ctx *c, uint64_t *out, int32_t n) {
+    if (!c || !out || n < 0) return fail(CCDGPU_EINVAL, "bad argument");
+    for (int i = 0; i < n && i < 32; ++i) out[i] = c->diag[i];
+    return 0;
 }
 
 int ccdgpu_last_stats(ccdgpu_ctx *c, ccdgpu_stats *s) {

@@ -1,0 +1,26 @@
+"""Per-phase cycle breakdown of the detection kernel (diagnostic build lib/libccdgpu_diag.so).
+Run on the GPU box:  python tools/phase_profile.py [config] [chips]"""
+import os, sys, json
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault('CCDGPU_LIBRARY', os.path.join(ROOT, 'lcmap-firebird_amd', 'lib', 'libccdgpu_diag.so'))
+sys.path.insert(0, os.path.join(ROOT, 'lcmap-firebird_amd'))
+import numpy as np
+import ccdgpu
+from ccdgpu import synth
+which = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+chips = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+cfg = synth.config(which)
+ids = [c for c in range(64) if synth.dates(cfg, c).shape[0] == synth.dates(cfg, 0).shape[0]][:chips]
+data = [synth.chip(cfg, c, 0, 10000) for c in ids]
+ctx = ccdgpu.Context(0)
+ctx.stage(np.stack([d[0] for d in data]), np.stack([d[1] for d in data]), np.stack([d[2] for d in data]))
+ctx.run()
+st, dc = ctx.stats(), ctx.diag_counters()
+names = ['pixel total', 'QA/filter/compact', 'variogram+peek', 'tmask', 'lasso gram', 'lasso cd',
+         'lasso rmse', 'closest-doy rmse', 'peek eval', 'outlier compaction', 'stability', 'medians+emit']
+tot = dc[8] or 1
+out = {'config': which, 'chips': chips, 'detect_ms': st['detect_ms'], 'fits': dc[0], 'sweeps': dc[1],
+       'sweeps_per_fit': dc[1] / max(1, dc[0] / 7)}
+for i, n in enumerate(names):
+    out[n] = dc[8 + i] / tot
+print(json.dumps(out, indent=1))
