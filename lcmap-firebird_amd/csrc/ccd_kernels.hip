@@ -41,8 +41,9 @@ constexpr int TR = 32;  // rows per LDS staging tile
 constexpr int MAXW = CCDGPU_MAX_OBS / 32;
 #define CCD_NPHASE 12
 
+static_assert(TR * RW >= CCDGPU_MAX_PEEK * 8, "row buffer holds the peek residuals");
 struct Lds {
-    double row[TR][RW];
+    double row[TR][RW];  // staging tile; also holds the last peek residuals (64 obs x 8 bands)
     double G[8][8];
     double Q[8][8];  // Q[j][band] = Xc_j . yc_band
     double YY[8];
@@ -151,7 +152,15 @@ __device__ __forceinline__ double wsum(double v) {
     v += dpp<0x140>(v);
     return (rdlane(v, 0) + rdlane(v, 16)) + (rdlane(v, 32) + rdlane(v, 48));
 }
-__device__ __forceinline__ void wsync() { __syncthreads(); }
+// wsync: order LDS traffic between the lanes of this (single-wave) workgroup -- the LDS
+// executes a wave's ds_* operations in order, so only compiler motion must be stopped.
+// gsync: hand-off of GLOBAL scratch written by one lane and read by another (compaction,
+// Tmask scratch): workgroup release/acquire (vmcnt drain) + barrier.
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+__device__ __forceinline__ void gsync() { __syncthreads(); }
 
 #define cvalf(P, b, j) ((double)CVR(P, b, j))
 
@@ -268,8 +277,7 @@ __device__ int compact_drop(Px &P, int a, F drop) {
         out += popc(keep);
     }
     P.m = out;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    wsync();
+    gsync();
     return out;
 }
 
@@ -817,8 +825,7 @@ __device__ int tmask(Px &P, int a, int b) {
            *wt = P.fs + 4 * P.n;
     if (ncol == 5) tm_trig(P, a, nw, oc, xoc, xos);
     for (int i = l; i < (nw + 31) / 32; i += W) L->tflag[i] = 0u;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    wsync();
+    gsync();
     // unweighted normal matrix: OLS solves and leverage h = diag(X (X'X)^-1 X') (robust_fit.RLM);
     // its Cholesky factor is kept in LDS (L->tchol) for the per-band OLS solves
     bool ok0;
@@ -914,6 +921,7 @@ __device__ int tmask(Px &P, int a, int b) {
                 wt[i] = fabs(u) < 4.685 ? om * om : 0.0;
             }
             double Gw[5][5], rw[5];
+            gsync();  // weights written lane-strided, read tile-strided
             tm_normal(P, a, nw, ncol, xoc, xos, band, wt);
             tm_load(&LDS(), Gw, rw);
             tm_solve(Gw, rw, coef);
@@ -1046,20 +1054,19 @@ __device__ bool eval_peek(Px &P, int k, int start, int dir, double &mag0) {
         const bool valid = jj < k && bnd < NB;
         double r = 0.0;
         if (valid) r = resid_at(P, bnd, start + dir * jj);
-        if (jj < k) P.fs[jj * 8 + bnd] = r;  // kept for the segment's magnitude medians
+        if (jj < k) (&L->row[0][0])[jj * 8 + bnd] = r;  // kept for the segment's magnitude medians
         const double v = r / rm;
         const double mag = gsum8((valid && det) ? v * v : 0.0);
         if (bal(bnd == 0 && jj < k && !(mag > P.chg))) all = false;
         if (pass == 0) mag0 = __shfl(mag, 0);
     }
     P.fl += (unsigned long long)k * (7 * 2 * 8 + 5 * 3);  // predict 7*2*8 + magnitude 5*3 per peek obs
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     wsync();
     return all;
 }
 
 // Median over the k peek residuals of each band (lookforward result magnitudes, taken from
-// the slot scratch where eval_peek left them); returns band l's median in lane l (l < 7).
+// the LDS row buffer where eval_peek left them); returns band l's median in lane l (l < 7).
 __device__ double peek_medians(Px &P, int k) {
     Lds *L = &LDS();
     const int l = lane();
@@ -1067,10 +1074,10 @@ __device__ double peek_medians(Px &P, int k) {
     const int t1 = (k - 1) / 2, t2 = k / 2;
     for (int jj = osub; jj < k; jj += 8) {
         if (bnd >= NB) continue;
-        const double v = P.fs[jj * 8 + bnd];
+        const double v = (&L->row[0][0])[jj * 8 + bnd];
         int rank = 0;
         for (int i = 0; i < k; ++i) {
-            const double u = P.fs[i * 8 + bnd];
+            const double u = (&L->row[0][0])[i * 8 + bnd];
             rank += (u < v || (u == v && i < jj)) ? 1 : 0;
         }
         if (rank == t1) L->med1[bnd] = v;
@@ -1383,8 +1390,7 @@ __device__ int px_setup(Px &P, int chip, int pix) {
         m += popc(k2);
     }
     P.m = m;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    wsync();
+    gsync();
     if (proc == CCDGPU_PROC_INSUFFICIENT_CLEAR && m > 0) {
         const int16_t *g = P.cv + (size_t)1 * n;
         auto gen = [&](int i, int &val) -> bool { val = (int)g[i] + 32768; return true; };
