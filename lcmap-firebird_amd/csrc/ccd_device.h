@@ -10,7 +10,7 @@
 //                                               (models/lasso.coefficient_matrix rows, shared by
 //                                                all 10^4 pixels of a chip)
 //   per wave slot scratch (persistent grid): compacted period of the current pixel
-//     cdate int32[n_obs], cidx uint16[n_obs], cval int16[7][n_obs]  (20 B / observation)
+//     cdate int32[n_obs], row {int16 v[7]; uint16 cidx}[n_obs]  (20 B / observation)
 //   outputs: mask bits, procedure, probs, per-pixel segment count, segment pool (+ seq numbers)
 #pragma once
 #include <stdint.h>
@@ -38,8 +38,7 @@ struct CcdDetectArgs {
     unsigned long long *counters;
     // per-slot scratch
     int32_t *s_date;
-    uint16_t *s_idx;
-    int16_t *s_val;
+    uint16_t *s_row;  // [n_slots][n_obs][8]: int16 band values 0..6, uint16 sorted index
     double *s_f64;   // [n_slots][8][n_obs] Tmask scratch / peek residuals
     // outputs
     uint32_t *mask_bits;
@@ -63,7 +62,12 @@ int ccdk_prep(const int64_t *dates, int32_t n_chips, int32_t n_obs, double avg_d
 // the detection kernel reads its arguments from a __constant__ symbol (one staged launch per
 // device at a time; the host API serialises launches per device)
 int ccdk_set_args(const CcdDetectArgs *host_args, void *stream);
-int ccdk_detect(int32_t grid, int variant, void *stream);
+int ccdk_detect(int32_t grid, int variant, int32_t n_obs, void *stream);
+// 1 if this build keeps the compacted period in LDS (-DCCD_PERIOD_IN_LDS)
+int ccdk_period_in_lds(void);
+// dynamic LDS bytes per wave and resident waves per CU for a period of n_obs observations
+size_t ccdk_lds_bytes(int32_t n_obs);
+int ccdk_occupancy(int variant, int32_t n_obs);
 int ccdk_scatter(const ccdgpu_segment *pool, const int32_t *pool_seq, int64_t n_pool,
                  const int64_t *offsets, int32_t n_pix_per_chip, ccdgpu_segment *out, void *stream);
 #ifdef __cplusplus

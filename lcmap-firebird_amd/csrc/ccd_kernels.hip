@@ -39,10 +39,17 @@ constexpr int W = CCD_WAVE;
 constexpr int RW = 16;  // doubles per staged design row: t c1 s1 c2 s2 c3 s3 _ y0..y6 _
 constexpr int TR = 32;  // rows per LDS staging tile
 constexpr int MAXW = CCDGPU_MAX_OBS / 32;
-#define CCD_NPHASE 12
+#define CCD_NPHASE 20
 
 static_assert(TR * RW >= CCDGPU_MAX_PEEK * 8, "row buffer holds the peek residuals");
-struct Lds {
+// Global-memory pointers kept in the per-pixel state are typed address_space(1) so every access
+// is a global_* instruction (a generic pointer would compile to flat_*, which also counts against
+// lgkmcnt and makes every later LDS wait wait for the global load too).
+#define GLOBAL_AS __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ GLOBAL_AS T *as_global(T *p) { return (GLOBAL_AS T *)p; }
+
+struct __attribute__((aligned(16))) Lds {
     double row[TR][RW];  // staging tile; also holds the last peek residuals (64 obs x 8 bands)
     double G[8][8];
     double Q[8][8];  // Q[j][band] = Xc_j . yc_band
@@ -67,17 +74,26 @@ __constant__ CcdDetectArgs c_args;
 extern __shared__ __attribute__((aligned(16))) char ccd_smem[];
 __device__ __forceinline__ Lds &LDS() { return *reinterpret_cast<Lds *>(ccd_smem); }
 
+// One compacted observation: the 7 band values and its sorted-date index in one 16-byte row, so a
+// random gather (closest-DOY, peek) touches one cache line instead of eight.
+struct __attribute__((aligned(16))) CRow {
+    int16_t v[NB];
+    uint16_t ci;
+};
+static_assert(sizeof(CRow) == 16, "CRow is one dwordx4");
+
 struct Px {
     int n;      // observations (sorted)
     int m;      // current compacted period length
     int peek;   // (adaptive) peek size
     double chg; // change threshold
-    const double *basis;
+    const GLOBAL_AS double *basis;
     const int64_t *sd;
-    int32_t *cd;
-    uint16_t *ci;
-    int16_t *cv;
-    double *fs;  // per-slot double scratch [8][n]
+#ifndef CCD_PERIOD_IN_LDS
+    int32_t *cd;  // compacted dates
+    CRow *cr;     // compacted rows: 7 band values + sorted index, one 16-byte load per observation
+#endif
+    GLOBAL_AS double *fs;  // per-slot double scratch [8][n]
     int64_t gpix;
     int nseg;
     unsigned long long fits, sweeps;
@@ -89,15 +105,34 @@ struct Px {
 #endif
 };
 
+// Where the compacted period lives.  CCD_PERIOD_IN_LDS: in the wave's LDS block right after the
+// Lds struct (dates, then rows at a 16-byte aligned offset) -- every period access is a ds_*
+// instruction; otherwise in the per-slot global scratch.
+#ifdef CCD_PERIOD_IN_LDS
+__device__ __forceinline__ int cd_bytes(int n) { return (4 * n + 15) & ~15; }
+__device__ __forceinline__ int32_t *PCD(const Px &) { return reinterpret_cast<int32_t *>(ccd_smem + sizeof(Lds)); }
+__device__ __forceinline__ CRow *PCR(const Px &P) {
+    return reinterpret_cast<CRow *>(ccd_smem + sizeof(Lds) + cd_bytes(P.n));
+}
+#else
+__device__ __forceinline__ int32_t *PCD(const Px &P) { return P.cd; }
+__device__ __forceinline__ CRow *PCR(const Px &P) { return P.cr; }
+#endif
+static_assert(sizeof(Lds) % 16 == 0, "period rows follow the Lds block 16-byte aligned");
+
 // ------------------------------------------------------------------ diagnostic phase timers
 // Built only into lib/libccdgpu_diag.so (-DCCD_PHASE_TIMERS): s_memtime cycle totals per phase,
 // summed over waves into stats[8 + phase].  Phases: 0 pixel total, 1 QA/filter/compaction,
 // 2 variogram + peek, 3 Tmask, 4 Lasso Gram, 5 Lasso CD, 6 Lasso rmse, 7 closest-DOY rmse,
-// 8 peek evaluation, 9 outlier compaction, 10 stability, 11 medians + emit.
+// 8 peek evaluation, 9 outlier compaction, 10 stability, 11 medians + emit; closest-DOY split:
+// 12 histogram build, 13 threshold scan, 14 selection scan, 15 residual gather; event counts:
+// 16 closest-DOY calls, 17 summed fit-window length, 18 peek evaluations, 19 fits.
 #ifdef CCD_PHASE_TIMERS
 #define PH_BEGIN(id) const unsigned long long _ph_##id = __builtin_amdgcn_s_memtime();
 #define PH_END(P, id, slot) (P).tph[slot] += __builtin_amdgcn_s_memtime() - _ph_##id;
+#define PH_COUNT(P, slot, v) (P).tph[slot] += (unsigned long long)(v);
 #else
+#define PH_COUNT(P, slot, v)
 #define PH_BEGIN(id)
 #define PH_END(P, id, slot)
 #endif
@@ -112,14 +147,20 @@ __device__ __forceinline__ int gidx(const Px &P, int j, int lim, int line) {
     P.bad = ok ? P.bad : line;
     return ok ? j : 0;
 }
-__device__ __forceinline__ int32_t cdr(const Px &P, int j, int line) { return P.cd[gidx(P, j, P.m, line)]; }
+__device__ __forceinline__ int32_t cdr(const Px &P, int j, int line) { return PCD(P)[gidx(P, j, P.m, line)]; }
 __device__ __forceinline__ int cir(const Px &P, int j, int line) {
-    const int c = P.ci[gidx(P, j, P.m, line)];
+    const int c = PCR(P)[gidx(P, j, P.m, line)].ci;
     return gidx(P, c, P.n, line);
 }
 __device__ __forceinline__ int16_t cvr(const Px &P, int b, int j, int line) {
-    return P.cv[(size_t)b * P.n + gidx(P, j, P.m, line)];
+    return PCR(P)[gidx(P, j, P.m, line)].v[b];
 }
+__device__ __forceinline__ CRow crow(const Px &P, int j, int line) {
+    CRow r = PCR(P)[gidx(P, j, P.m, line)];
+    r.ci = (uint16_t)gidx(P, r.ci, P.n, line);
+    return r;
+}
+#define CROW(P, j) crow(P, (j), __LINE__)
 #define CDR(P, j) cdr(P, (j), __LINE__)
 #define CIR(P, j) cir(P, (j), __LINE__)
 #define CVR(P, b, j) cvr(P, (b), (j), __LINE__)
@@ -144,6 +185,21 @@ __device__ __forceinline__ double rdlane(double v, int l) {
     return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
                             __builtin_amdgcn_readlane(__double2loint(v), l));
 }
+// Inclusive prefix sum over the 64 lanes in DPP only (no LDS round trip): Hillis-Steele with
+// row_shr 1/2/4/8 inside each row of 16, then row_bcast:15 (rows 1, 3) and row_bcast:31
+// (rows 2, 3) carry the row totals across.
+__device__ __forceinline__ int wscan_incl(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);
+    return v;
+}
+// value of v in a (wave-uniform) lane, as a scalar
+__device__ __forceinline__ int rdl(int v, int src) { return __builtin_amdgcn_readlane(v, src); }
+
 // wave-wide sum, identical (wave-uniform) result in every lane
 __device__ __forceinline__ double wsum(double v) {
     v += dpp<0xB1>(v);
@@ -161,12 +217,18 @@ __device__ __forceinline__ void wsync() {
     __builtin_amdgcn_wave_barrier();
 }
 __device__ __forceinline__ void gsync() { __syncthreads(); }
+// psync: hand-off of compacted-period data written by one lane and read by another
+#ifdef CCD_PERIOD_IN_LDS
+__device__ __forceinline__ void psync() { wsync(); }
+#else
+__device__ __forceinline__ void psync() { gsync(); }
+#endif
 
 #define cvalf(P, b, j) ((double)CVR(P, b, j))
 
 // k-th smallest (0-based) of integer values in [lo, hi] produced by gen(i, &v) (returns valid).
 template <class F>
-__device__ int kth_int(F gen, int N, int k, int lo, int hi) {
+__device__ __forceinline__ int kth_int(F gen, int N, int k, int lo, int hi) {
     const int l = lane();
     while (lo < hi) {
         const int mid = lo + ((hi - lo) >> 1);
@@ -185,7 +247,7 @@ __device__ int kth_int(F gen, int N, int k, int lo, int hi) {
 }
 
 template <class F>
-__device__ double median_int(F gen, int N, int cnt, int lo, int hi) {
+__device__ __forceinline__ double median_int(F gen, int N, int cnt, int lo, int hi) {
     if (cnt <= 0) return __builtin_nan("");
     if (cnt & 1) return (double)kth_int(gen, N, cnt / 2, lo, hi);
     const int a = kth_int(gen, N, cnt / 2 - 1, lo, hi);
@@ -194,7 +256,7 @@ __device__ double median_int(F gen, int N, int cnt, int lo, int hi) {
 }
 
 // k-th smallest of non-negative doubles vals[0..N) (bit patterns are monotone for x >= 0).
-__device__ double kth_nonneg(const double *vals, int N, int k) {
+__device__ __forceinline__ double kth_nonneg(const GLOBAL_AS double *vals, int N, int k) {
     const int l = lane();
     unsigned long long lo = 0ull, hi = 0x7FF0000000000000ull;
     while (lo < hi) {
@@ -248,36 +310,32 @@ __device__ __forceinline__ int qabitval(const ccdgpu_params &p, unsigned v) {
 // Drop observations of [a, m) for which drop(j) is true (j = compacted index, valid only for the
 // caller's range); the tail is shifted down in one ascending pass (writes never overtake reads).
 template <class F>
-__device__ int compact_drop(Px &P, int a, F drop) {
+__device__ __forceinline__ int compact_drop(Px &P, int a, F drop) {
     const int l = lane();
     int out = a;
     for (int base = a; base < P.m; base += W) {
         const int j = base + l;
         const bool in = j < P.m;
         int32_t d = 0;
-        uint16_t c = 0;
-        int16_t v[NB];
+        uint4 r = {0u, 0u, 0u, 0u};  // the 16-byte row as one vector (ci = high half of .w)
         bool dr = false;
         if (in) {
-            d = P.cd[j];
-            c = P.ci[j];
-#pragma unroll
-            for (int b = 0; b < NB; ++b) v[b] = P.cv[(size_t)b * P.n + j];
+            d = PCD(P)[j];
+            r = reinterpret_cast<const uint4 *>(PCR(P))[j];
             dr = drop(j);
         }
         const unsigned long long keep = bal(in && !dr);
-        if (in && dr) atomicAnd(&LDS().mask[c >> 5], ~(1u << (c & 31)));
+        const unsigned ci = r.w >> 16;
+        if (in && dr) atomicAnd(&LDS().mask[ci >> 5], ~(1u << (ci & 31)));
         if (in && !dr) {
             const int pos = gidx(P, out + below(keep), P.n, __LINE__);
-            P.cd[pos] = d;
-            P.ci[pos] = c;
-#pragma unroll
-            for (int b = 0; b < NB; ++b) P.cv[(size_t)b * P.n + pos] = v[b];
+            PCD(P)[pos] = d;
+            reinterpret_cast<uint4 *>(PCR(P))[pos] = r;
         }
         out += popc(keep);
     }
     P.m = out;
-    gsync();
+    psync();
     return out;
 }
 
@@ -286,13 +344,13 @@ __device__ __forceinline__ void stage_rows(const Px &P, int j0, int cnt) {
     const int l = lane();
     if (l < cnt) {
         const int j = j0 + l;
-        const double *bs = P.basis + (size_t)CIR(P, j) * CCD_BASIS_STRIDE;
+        const CRow cw = CROW(P, j);
+        const GLOBAL_AS double *bs = P.basis + (size_t)cw.ci * CCD_BASIS_STRIDE;
         double *r = LDS().row[l];
-        r[0] = (double)CDR(P, j);
 #pragma unroll
-        for (int c = 1; c < 7; ++c) r[c] = bs[c];
+        for (int c = 0; c < 7; ++c) r[c] = bs[c];  // bs[0] = t
 #pragma unroll
-        for (int b = 0; b < NB; ++b) r[8 + b] = cvalf(P, b, j);
+        for (int b = 0; b < NB; ++b) r[8 + b] = (double)cw.v[b];
     }
     wsync();
 }
@@ -316,7 +374,7 @@ __device__ __forceinline__ double gmax8(double v) {
 // 7 bands at once: lane = band * 8 + coordinate.  Lane (b, k) holds Gram column k, q_k = Xc_k.yc_b
 // and w_k; the partial sum of coordinate j's update is an 8-lane butterfly.  Writes
 // L->coef[b][0..6]; returns the sweep count (every lane of the band's group).
-__device__ int cd_lanes(Lds *L, int pc, double alpha, int max_iter, double tol) {
+__device__ __forceinline__ int cd_lanes(Lds *L, int pc, double alpha, int max_iter, double tol) {
     const int l = lane();
     const int b = l >> 3, k = l & 7;
     const bool act = b < NB && k < pc;
@@ -385,17 +443,19 @@ __device__ int cd_lanes(Lds *L, int pc, double alpha, int max_iter, double tol) 
 
 // residual of band b at compacted observation j for the current models (lasso.predict)
 __device__ __forceinline__ double resid_at(const Px &P, int band, int j) {
-    const double *bs = P.basis + (size_t)CIR(P, j) * CCD_BASIS_STRIDE;
+    const int g = gidx(P, j, P.m, __LINE__);
+    const CRow *rw = PCR(P) + g;  // band value and index read in place (no dynamically indexed copy)
+    const GLOBAL_AS double *bs = P.basis + (size_t)gidx(P, rw->ci, P.n, __LINE__) * CCD_BASIS_STRIDE;
     const double *c = LDS().coef[band];
-    double pr = (double)CDR(P, j) * c[0];
+    double pr = bs[0] * c[0];  // bs[0] = (double) date
 #pragma unroll
     for (int jj = 1; jj < 7; ++jj) pr += bs[jj] * c[jj];
     pr += c[7];
-    return cvalf(P, band, j) - pr;
+    return (double)rw->v[band] - pr;
 }
 
 // lasso.fitted_model for the 7 bands over compacted window [a, b) with k coefficients.
-__device__ void fit_models(Px &P, int a, int b, int k) {
+__device__ __forceinline__ void fit_models(Px &P, int a, int b, int k) {
     const ccdgpu_params &p = c_args.p;
     Lds *L = &LDS();
     const int l = lane();
@@ -495,18 +555,16 @@ __device__ void fit_models(Px &P, int a, int b, int k) {
     // rmse from residuals of the raw design (predict = X @ coef + intercept);
     // lane = (observation sub-index, band), 8 observations per pass
     {
-        const int bnd = l & 7, osub = l >> 3;
+        const int bnd = l >> 3, osub = l & 7;  // band-major: DPP reduction over the 8 partials
         double ss = 0.0;
         if (bnd < NB)
             for (int t0 = osub; t0 < nw; t0 += 8) {
                 const double r = resid_at(P, bnd, a + t0);
                 ss += r * r;
             }
-        ss += __shfl_xor(ss, 8);
-        ss += __shfl_xor(ss, 16);
-        ss += __shfl_xor(ss, 32);
+        ss = gsum8(ss);
         const double den = (double)(nw - (p.rmse_dof ? k : 0));
-        if (l < NB) L->rmse[l] = sqrt(ss / den);
+        if (osub == 0 && bnd < NB) L->rmse[bnd] = sqrt(ss / den);
     }
     wsync();
     PH_END(P, rmse, 6)
@@ -514,7 +572,7 @@ __device__ void fit_models(Px &P, int a, int b, int k) {
 
 
 // ------------------------------------------------------------------ segment output
-__device__ void emit(Px &P, int sday, int eday, int bday, int count, double chprob, int cqa,
+__device__ __forceinline__ void emit(Px &P, int sday, int eday, int bday, int count, double chprob, int cqa,
                      double mag_lane /* lane b: magnitude of band b */) {
     const CcdDetectArgs &A = c_args;
     const int l = lane();
@@ -547,7 +605,7 @@ __device__ void emit(Px &P, int sday, int eday, int bday, int count, double chpr
     P.nseg++;
 }
 
-__device__ void catch_(Px &P, int a, int b, int cqa) {
+__device__ __forceinline__ void catch_(Px &P, int a, int b, int cqa) {
     fit_models(P, a, b, c_args.p.coef_min);
     const int bday = b < P.m ? CDR(P, b) : CDR(P, P.m - 1);
     emit(P, CDR(P, a), CDR(P, b - 1), bday, b - a, 0.0, cqa, 0.0);
@@ -556,7 +614,7 @@ __device__ void catch_(Px &P, int a, int b, int cqa) {
 // k-th smallest (0-based) of 16-bit unsigned values produced by gen(i, &v) for i < N (valid if
 // gen returns true): two-pass radix select over 256-bin LDS histograms (L->hist2 as scratch).
 template <class F>
-__device__ int select_u16(F gen, int N, int k) {
+__device__ __forceinline__ int select_u16(F gen, int N, int k) {
     Lds *L = &LDS();
     const int l = lane();
     int hiB = 0, rank = k;
@@ -574,21 +632,15 @@ __device__ int select_u16(F gen, int N, int k) {
         int carry = 0, found = -1;
         for (int b0 = 0; b0 < 256; b0 += W) {
             const int c = (int)L->hist2[b0 + l];
-            int cum = c;
-#pragma unroll
-            for (int o = 1; o < W; o <<= 1) {
-                const int t = __shfl_up(cum, o);
-                if (l >= o) cum += t;
-            }
-            cum += carry;
+            const int cum = wscan_incl(c) + carry;
             const unsigned long long hit = bal(cum > rank);
             if (hit) {
                 const int src = __ffsll((long long)hit) - 1;
                 found = b0 + src;
-                rank -= __shfl(cum, src) - __shfl(c, src);
+                rank -= rdl(cum, src) - rdl(c, src);
                 break;
             }
-            carry = __shfl(cum, W - 1);
+            carry = rdl(cum, W - 1);
         }
         wsync();
         if (pass == 0) hiB = found;
@@ -598,7 +650,7 @@ __device__ int select_u16(F gen, int N, int k) {
 }
 
 template <class F>
-__device__ double median_u16(F gen, int N, int cnt) {
+__device__ __forceinline__ double median_u16(F gen, int N, int cnt) {
     if (cnt <= 0) return __builtin_nan("");
     if (cnt & 1) return (double)select_u16(gen, N, cnt / 2);
     const int a = select_u16(gen, N, cnt / 2 - 1);
@@ -607,7 +659,7 @@ __device__ double median_u16(F gen, int N, int cnt) {
 }
 
 // ------------------------------------------------------------------ variogram / peek
-__device__ void variogram(Px &P) {
+__device__ __forceinline__ void variogram(Px &P) {
     Lds *L = &LDS();
     const int l = lane();
     const int m = P.m;
@@ -633,11 +685,11 @@ __device__ void variogram(Px &P) {
         cnt += popc(bal(i < m - kk && (all || (CDR(P, i + kk) - CDR(P, i)) > 30)));
     }
     for (int band = 0; band < NB; ++band) {
-        const int16_t *v = P.cv + (size_t)band * P.n;
+        const CRow *v = PCR(P);
         auto gen = [&](int i, int &val) -> bool {
             if (i >= m - kk) return false;
             if (!all && (CDR(P, i + kk) - CDR(P, i)) <= 30) return false;
-            int d = (int)v[i + kk] - (int)v[i];
+            int d = (int)v[i + kk].v[band] - (int)v[i].v[band];
             val = d < 0 ? -d : d;
             return true;
         };
@@ -648,7 +700,7 @@ __device__ void variogram(Px &P) {
     wsync();
 }
 
-__device__ void adjust_peek(Px &P) {
+__device__ __forceinline__ void adjust_peek(Px &P) {
     const ccdgpu_params &p = c_args.p;
     P.peek = p.peek_size;
     P.chg = p.change_threshold;
@@ -670,9 +722,9 @@ __device__ void adjust_peek(Px &P) {
 // Tmask design row: [cos wt, sin wt, cos (w/N) t, sin (w/N) t, 1]; when N = 1 the annual and the
 // observation cycle coincide (rank-deficient 5-column design) and the row is [cos, sin, 1, 0, 0]
 // with the two unused normal-matrix diagonals pinned to 1 (Tmask).
-__device__ __forceinline__ void tm_row(const Px &P, int j, int i, int ncol, const double *xoc,
-                                       const double *xos, double (&x)[5]) {
-    const double *bs = P.basis + (size_t)CIR(P, j) * CCD_BASIS_STRIDE;
+__device__ __forceinline__ void tm_row(const Px &P, int j, int i, int ncol, const GLOBAL_AS double *xoc,
+                                       const GLOBAL_AS double *xos, double (&x)[5]) {
+    const GLOBAL_AS double *bs = P.basis + (size_t)CIR(P, j) * CCD_BASIS_STRIDE;
     x[0] = bs[1];
     x[1] = bs[2];
     if (ncol == 5) {
@@ -689,8 +741,8 @@ __device__ __forceinline__ void tm_row(const Px &P, int j, int i, int ncol, cons
 // normal equations sum w x x^T and sum w x y over the window into L->G[0..4][0..4] and
 // L->Q[0..4][0]: rows [x0..x4, w, y] staged in LDS 64 at a time, lane = matrix entry,
 // sequential over rows (same scheme as the Lasso Gram in fit_models).
-__device__ void tm_normal(const Px &P, int a, int nw, int ncol, const double *xoc,
-                                       const double *xos, int band, const double *wv) {
+__device__ __forceinline__ void tm_normal(const Px &P, int a, int nw, int ncol, const GLOBAL_AS double *xoc,
+                                       const GLOBAL_AS double *xos, int band, const GLOBAL_AS double *wv) {
     Lds *L = &LDS();
     const int l = lane();
     int ea = -1, eb = -1;
@@ -792,8 +844,8 @@ __device__ __forceinline__ void tm_solve(double (&A)[5][5], const double (&rhs)[
     }
 }
 
-__device__ __forceinline__ double tm_pred(const Px &P, int j, int i, int ncol, const double *xoc,
-                                          const double *xos, const double (&coef)[5]) {
+__device__ __forceinline__ double tm_pred(const Px &P, int j, int i, int ncol, const GLOBAL_AS double *xoc,
+                                          const GLOBAL_AS double *xos, const double (&coef)[5]) {
     double x[5];
     tm_row(P, j, i, ncol, xoc, xos, x);
     double pr = 0.0;
@@ -803,7 +855,7 @@ __device__ __forceinline__ double tm_pred(const Px &P, int j, int i, int ncol, c
 }
 
 // cos / sin of the observation-cycle harmonic (w / N) t for the window (lane = obs)
-__device__ void tm_trig(const Px &P, int a, int nw, double oc, double *xoc, double *xos) {
+__device__ __forceinline__ void tm_trig(const Px &P, int a, int nw, double oc, GLOBAL_AS double *xoc, GLOBAL_AS double *xos) {
     for (int i = lane(); i < nw; i += W) {
         double sv, cv;
         sincos(oc * (double)CDR(P, a + i), &sv, &cv);
@@ -813,7 +865,7 @@ __device__ void tm_trig(const Px &P, int a, int nw, double oc, double *xoc, doub
 }
 
 // Returns the outlier count; outlier flags in L->tflag (bit i = window observation i).
-__device__ int tmask(Px &P, int a, int b) {
+__device__ __forceinline__ int tmask(Px &P, int a, int b) {
     const ccdgpu_params &p = c_args.p;
     Lds *L = &LDS();
     const int l = lane();
@@ -821,7 +873,7 @@ __device__ int tmask(Px &P, int a, int b) {
     const double w = 2.0 * M_PI / p.avg_days_yr;
     const double oc = w / ceil(((double)CDR(P, b - 1) - (double)CDR(P, a)) / p.avg_days_yr);
     const int ncol = (oc == w) ? 3 : 5;
-    double *xoc = P.fs, *xos = P.fs + P.n, *adj = P.fs + 2 * P.n, *absr = P.fs + 3 * P.n,
+    GLOBAL_AS double *xoc = P.fs, *xos = P.fs + P.n, *adj = P.fs + 2 * P.n, *absr = P.fs + 3 * P.n,
            *wt = P.fs + 4 * P.n;
     if (ncol == 5) tm_trig(P, a, nw, oc, xoc, xos);
     for (int i = l; i < (nw + 31) / 32; i += W) L->tflag[i] = 0u;
@@ -965,7 +1017,7 @@ __device__ __forceinline__ int num_coefs(const ccdgpu_params &p, int n) {
     return p.coef_max;
 }
 
-__device__ bool stable(const Px &P, int a, int b) {
+__device__ __forceinline__ bool stable(const Px &P, int a, int b) {
     const ccdgpu_params &p = c_args.p;
     const Lds *L = &LDS();
     const int l = lane();
@@ -982,7 +1034,7 @@ __device__ bool stable(const Px &P, int a, int b) {
 }
 __device__ __forceinline__ void count_stable(Px &P) {}
 
-__device__ bool initialize(Px &P, int &wa, int &wb) {
+__device__ __forceinline__ bool initialize(Px &P, int &wa, int &wb) {
     const ccdgpu_params &p = c_args.p;
     const Lds *L = &LDS();
     const int l = lane();
@@ -1034,7 +1086,7 @@ __device__ bool initialize(Px &P, int &wa, int &wb) {
 // (change.change_magnitude) reduced over the 8 band lanes.  rl[pass] keeps each lane's residual
 // for the segment's magnitude medians.  Returns true iff every peek observation exceeds the
 // change threshold (change.detect_change); mag0 = magnitude of observation 0 (detect_outlier).
-__device__ bool eval_peek(Px &P, int k, int start, int dir, double &mag0) {
+__device__ __forceinline__ bool eval_peek(Px &P, int k, int start, int dir, double &mag0) {
     const ccdgpu_params &p = c_args.p;
     Lds *L = &LDS();
     const int l = lane();
@@ -1047,27 +1099,36 @@ __device__ bool eval_peek(Px &P, int k, int start, int dir, double &mag0) {
     }
     bool all = true;
     mag0 = 0.0;
+    // gathers of up to 4 rounds first (all in flight together), then the magnitudes
+    double rr[4];
+#pragma unroll
+    for (int pass = 0; pass < 4; ++pass) {
+        const int jj = pass * 8 + osub;
+        rr[pass] = (pass * 8 < k && jj < k && bnd < NB) ? resid_at(P, bnd, start + dir * jj) : 0.0;
+    }
 #pragma unroll
     for (int pass = 0; pass < 8; ++pass) {
         if (pass * 8 >= k) break;
         const int jj = pass * 8 + osub;
         const bool valid = jj < k && bnd < NB;
         double r = 0.0;
-        if (valid) r = resid_at(P, bnd, start + dir * jj);
+        if (pass < 4) r = rr[pass < 4 ? pass : 0];
+        else if (valid) r = resid_at(P, bnd, start + dir * jj);
         if (jj < k) (&L->row[0][0])[jj * 8 + bnd] = r;  // kept for the segment's magnitude medians
         const double v = r / rm;
         const double mag = gsum8((valid && det) ? v * v : 0.0);
         if (bal(bnd == 0 && jj < k && !(mag > P.chg))) all = false;
         if (pass == 0) mag0 = __shfl(mag, 0);
     }
-    P.fl += (unsigned long long)k * (7 * 2 * 8 + 5 * 3);  // predict 7*2*8 + magnitude 5*3 per peek obs
+    P.fl += (unsigned long long)k * (7 * 2 * 8 + 5 * 3);
+    PH_COUNT(P, 18, 1)  // predict 7*2*8 + magnitude 5*3 per peek obs
     wsync();
     return all;
 }
 
 // Median over the k peek residuals of each band (lookforward result magnitudes, taken from
 // the LDS row buffer where eval_peek left them); returns band l's median in lane l (l < 7).
-__device__ double peek_medians(Px &P, int k) {
+__device__ __forceinline__ double peek_medians(Px &P, int k) {
     Lds *L = &LDS();
     const int l = lane();
     const int bnd = l & 7, osub = l >> 3;
@@ -1090,7 +1151,7 @@ __device__ double peek_medians(Px &P, int k) {
     return out;
 }
 
-__device__ void lookback(Px &P, int &wa, int &wb, int prev) {
+__device__ __forceinline__ void lookback(Px &P, int &wa, int &wb, int prev) {
     const ccdgpu_params &p = c_args.p;
     const int l = lane();
     int a = wa, b = wb;
@@ -1131,7 +1192,7 @@ __device__ void lookback(Px &P, int &wa, int &wb, int prev) {
 __device__ __forceinline__ int u1461(int t) { return (4 * t) % 1461; }
 __device__ __forceinline__ int hbin(const Lds *L, int u) { return (int)((L->hist2[u >> 1] >> ((u & 1) * 16)) & 0xFFFFu); }
 
-__device__ void build_hist(const Px &P, int fa, int fb) {
+__device__ __forceinline__ void build_hist(const Px &P, int fa, int fb) {
     Lds *L = &LDS();
     const int l = lane();
     for (int i = l; i < 732; i += W) L->hist2[i] = 0u;
@@ -1143,12 +1204,15 @@ __device__ void build_hist(const Px &P, int fa, int fb) {
     wsync();
 }
 
-__device__ void closest_doy_comp(Px &P, int fa, int fb, int ref_idx) {
+__device__ __forceinline__ void closest_doy_comp(Px &P, int fa, int fb, int ref_idx) {
     Lds *L = &LDS();
     const int l = lane();
     const int nf = fb - fa;
     const int ur = u1461(CDR(P, ref_idx));
     int K = 1 << 20, need = 0;
+    PH_COUNT(P, 16, 1)
+    PH_COUNT(P, 17, nf)
+    PH_BEGIN(ts)
     if (nf > 24) {
         int carry = 0;
         for (int base = 0; base <= 730; base += W) {
@@ -1156,23 +1220,19 @@ __device__ void closest_doy_comp(Px &P, int fa, int fb, int ref_idx) {
             int c = 0;
             if (dd == 0) c = hbin(L, ur);
             else if (dd <= 730) c = hbin(L, (ur + dd) % 1461) + hbin(L, (ur - dd + 1461) % 1461);
-            int cum = c;
-#pragma unroll
-            for (int o = 1; o < W; o <<= 1) {
-                const int t = __shfl_up(cum, o);
-                if (l >= o) cum += t;
-            }
-            cum += carry;
+            const int cum = wscan_incl(c) + carry;
             const unsigned long long hit = bal(cum >= 24);
             if (hit) {
                 const int src = __ffsll((long long)hit) - 1;
                 K = base + src;
-                need = 24 - (__shfl(cum, src) - __shfl(c, src));
+                need = 24 - (rdl(cum, src) - rdl(c, src));
                 break;
             }
-            carry = __shfl(cum, W - 1);
+            carry = rdl(cum, W - 1);
         }
     }
+    PH_END(P, ts, 13)
+    PH_BEGIN(ss)
     int taken_eq = 0, nsel = 0;
     for (int t0 = 0; t0 < nf; t0 += W) {
         const int i = t0 + l;
@@ -1190,22 +1250,28 @@ __device__ void closest_doy_comp(Px &P, int fa, int fb, int ref_idx) {
         nsel += popc(sm);
     }
     wsync();
-    const int bnd = l & 7, osub = l >> 3;
-    double ss = 0.0;
-    if (bnd < NB)
-        for (int s2 = osub; s2 < nsel; s2 += 8) {
-            const double e = resid_at(P, bnd, L->sel[s2]);
-            ss += e * e;
-        }
-    ss += __shfl_xor(ss, 8);
-    ss += __shfl_xor(ss, 16);
-    ss += __shfl_xor(ss, 32);
-    if (l < NB) L->comp[l] = sqrt(ss) / 4.0;
+    PH_END(P, ss, 14)
+    PH_BEGIN(rg)
+    const int bnd = l >> 3, osub = l & 7;  // band-major: a band's 8 partial sums share a DPP row
+    // nsel <= 24: three fixed rounds of 8 observations, unrolled so the row / basis gathers of
+    // all three are in flight together
+    double e[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const int s2 = osub + 8 * r;
+        e[r] = (bnd < NB && s2 < nsel) ? resid_at(P, bnd, L->sel[s2]) : 0.0;
+    }
+    double ss = e[0] * e[0];
+    ss += e[1] * e[1];
+    ss += e[2] * e[2];
+    ss = gsum8(ss);
+    if (osub == 0 && bnd < NB) L->comp[bnd] = sqrt(ss) / 4.0;
     wsync();
+    PH_END(P, rg, 15)
     P.fl += (unsigned long long)nf * 6 + 5 * 48;  // closest-DOY keys 6 n_fit + comparison rmse 5 * 48
 }
 
-__device__ void lookforward(Px &P, int &wa, int &wb) {
+__device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
     const ccdgpu_params &p = c_args.p;
     const int l = lane();
     int a = wa, b = wb;
@@ -1221,24 +1287,23 @@ __device__ void lookforward(Px &P, int &wa, int &wb) {
         peek_start = b;
         const int k = P.peek;
         const double model_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
-        if (!have || b - a < 24) {
+        const bool early = !have || b - a < 24;  // refit every step, comparison rmse = model rmse
+        if (early || model_span >= 1.33 * fit_span) {
             fa = a;
             fb = b;
             fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
             fit_models(P, fa, fb, nc);
             have = true;
+        }
+        if (early) {
             if (l < NB) LDS().comp[l] = LDS().rmse[l];
             wsync();
         } else {
-            if (model_span >= 1.33 * fit_span) {
-                fa = a;
-                fb = b;
-                fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
-                fit_models(P, fa, fb, nc);
-            }
             PH_BEGIN(cl)
             if (fb - fa > 24 && (hfa != fa || hfb != fb)) {
+                PH_BEGIN(hb)
                 build_hist(P, fa, fb);
+                PH_END(P, hb, 12)
                 hfa = fa;
                 hfb = fb;
             }
@@ -1270,7 +1335,7 @@ __device__ void lookforward(Px &P, int &wa, int &wb) {
     wb = b;
 }
 
-__device__ void standard_procedure(Px &P) {
+__device__ __forceinline__ void standard_procedure(Px &P) {
     const ccdgpu_params &p = c_args.p;
     const int meow = p.meow_size;
     PH_BEGIN(vg)
@@ -1300,7 +1365,7 @@ __device__ void standard_procedure(Px &P) {
 
 // ------------------------------------------------------------------ qa.py filters + compaction
 // Returns the procedure, or -1 for an unsupported QA value.
-__device__ int px_setup(Px &P, int chip, int pix) {
+__device__ __forceinline__ int px_setup(Px &P, int chip, int pix) {
     const CcdDetectArgs &A = c_args;
     const ccdgpu_params &p = A.p;
     Lds *L = &LDS();
@@ -1378,10 +1443,12 @@ __device__ int px_setup(Px &P, int chip, int pix) {
         const unsigned long long k2 = bal(keep2);
         if (keep2) {
             const int pos = gidx(P, m + below(k2), n, __LINE__);
-            P.cd[pos] = d;
-            P.ci[pos] = (uint16_t)i;
+            PCD(P)[pos] = d;
+            CRow cw;
 #pragma unroll
-            for (int b = 0; b < NB; ++b) P.cv[(size_t)b * n + pos] = v[b];
+            for (int b = 0; b < NB; ++b) cw.v[b] = v[b];
+            cw.ci = (uint16_t)i;
+            PCR(P)[pos] = cw;
         }
         if (l == 0) {
             L->mask[base >> 5] = (unsigned)k2;
@@ -1390,12 +1457,12 @@ __device__ int px_setup(Px &P, int chip, int pix) {
         m += popc(k2);
     }
     P.m = m;
-    gsync();
+    psync();
     if (proc == CCDGPU_PROC_INSUFFICIENT_CLEAR && m > 0) {
-        const int16_t *g = P.cv + (size_t)1 * n;
-        auto gen = [&](int i, int &val) -> bool { val = (int)g[i] + 32768; return true; };
+        const CRow *g = PCR(P);
+        auto gen = [&](int i, int &val) -> bool { val = (int)g[i].v[1] + 32768; return true; };
         const double med = median_u16(gen, m, m) - 32768.0 + (double)p.median_green_filter;
-        compact_drop(P, 0, [&](int j) { return !((double)g[j] < med); });
+        compact_drop(P, 0, [&](int j) { return !((double)g[j].v[1] < med); });
     }
     return proc;
 }
@@ -1407,10 +1474,11 @@ __device__ __forceinline__ void detect_body() {
     const int slot = blockIdx.x;
     Px P;
     P.n = A.n_obs;
+#ifndef CCD_PERIOD_IN_LDS
     P.cd = A.s_date + (size_t)slot * A.n_obs;
-    P.ci = A.s_idx + (size_t)slot * A.n_obs;
-    P.cv = A.s_val + (size_t)slot * NB * A.n_obs;
-    P.fs = A.s_f64 + (size_t)slot * 8 * A.n_obs;
+    P.cr = reinterpret_cast<CRow *>(A.s_row) + (size_t)slot * A.n_obs;
+#endif
+    P.fs = as_global(A.s_f64 + (size_t)slot * 8 * A.n_obs);
     P.fits = 0;
     P.sweeps = 0;
     P.bad = 0;
@@ -1428,7 +1496,7 @@ __device__ __forceinline__ void detect_body() {
         const int pix = (int)(job % (unsigned long long)A.n_pix);
         P.gpix = (int64_t)job;
         P.nseg = 0;
-        P.basis = A.basis + (size_t)chip * A.n_obs * CCD_BASIS_STRIDE;
+        P.basis = as_global(A.basis + (size_t)chip * A.n_obs * CCD_BASIS_STRIDE);
         P.sd = A.sdates + (size_t)chip * A.n_obs;
         PH_BEGIN(tot)
         PH_BEGIN(su)
@@ -1486,8 +1554,8 @@ __device__ __forceinline__ void detect_body() {
 
 // Two register budgets of the same body: occupancy-1 (no spills) and 4 waves/SIMD (128 VGPRs,
 // the compiler spills the rest).  The host picks one (CCDGPU_KERNEL=w1|w4; default w4).
-__global__ __launch_bounds__(64) void ccd_detect() { detect_body(); }
-__global__ __launch_bounds__(64, 4) void ccd_detect_w4() { detect_body(); }
+__global__ __launch_bounds__(64) __attribute__((flatten)) void ccd_detect() { detect_body(); }
+__global__ __launch_bounds__(64, 4) __attribute__((flatten)) void ccd_detect_w4() { detect_body(); }
 
 // ------------------------------------------------------------------ per-chip preparation
 // One 256-thread block per chip: stable rank of each date (ties by input position), sorted
@@ -1558,11 +1626,43 @@ extern "C" int ccdk_set_args(const CcdDetectArgs *host_args, void *stream) {
                                   hipMemcpyHostToDevice, (hipStream_t)stream) == hipSuccess ? 0 : -1;
 }
 
-extern "C" int ccdk_detect(int32_t grid, int variant, void *stream) {
+extern "C" int ccdk_period_in_lds(void) {
+#ifdef CCD_PERIOD_IN_LDS
+    return 1;
+#else
+    return 0;
+#endif
+}
+
+extern "C" size_t ccdk_lds_bytes(int32_t n_obs) {
+#ifdef CCD_PERIOD_IN_LDS
+    return sizeof(Lds) + (size_t)((4 * n_obs + 15) & ~15) + sizeof(CRow) * (size_t)n_obs;
+#else
+    (void)n_obs;
+    return sizeof(Lds);
+#endif
+}
+
+static const void *detect_fn(int variant) {
+    return variant == 1 ? reinterpret_cast<const void *>(&ccd_detect) : reinterpret_cast<const void *>(&ccd_detect_w4);
+}
+
+// resident waves per CU for this variant and period length (0 on error)
+extern "C" int ccdk_occupancy(int variant, int32_t n_obs) {
+    const size_t lds = ccdk_lds_bytes(n_obs);
+    if (hipFuncSetAttribute(detect_fn(variant), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return 0;
+    int blocks = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, detect_fn(variant), 64, lds) != hipSuccess) return 0;
+    return blocks;
+}
+
+extern "C" int ccdk_detect(int32_t grid, int variant, int32_t n_obs, void *stream) {
+    const size_t lds = ccdk_lds_bytes(n_obs);
     if (variant == 1)
-        hipLaunchKernelGGL(ccd_detect, dim3(grid), dim3(64), sizeof(Lds), (hipStream_t)stream);
+        hipLaunchKernelGGL(ccd_detect, dim3(grid), dim3(64), lds, (hipStream_t)stream);
     else
-        hipLaunchKernelGGL(ccd_detect_w4, dim3(grid), dim3(64), sizeof(Lds), (hipStream_t)stream);
+        hipLaunchKernelGGL(ccd_detect_w4, dim3(grid), dim3(64), lds, (hipStream_t)stream);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -96,8 +96,7 @@ struct ccdgpu_ctx {
     DevBuf<double> basis, probs, s_f64;
     DevBuf<unsigned long long> counters, stats;
     DevBuf<int32_t> s_date;
-    DevBuf<uint16_t> s_idx;
-    DevBuf<int16_t> s_val;
+    DevBuf<uint16_t> s_row;
     DevBuf<uint32_t> mask;
     DevBuf<ccdgpu_segment> pool, csr;
     DevBuf<CcdDetectArgs> args;
@@ -113,8 +112,7 @@ struct ccdgpu_ctx {
         for (auto *b : {&basis, &probs, &s_f64}) b->release();
         counters.release();
         stats.release();
-        s_idx.release();
-        s_val.release();
+        s_row.release();
         mask.release();
         pool.release();
         csr.release();
@@ -214,6 +212,7 @@ int ccdgpu_init(int device, ccdgpu_ctx **out) {
     }
     for (auto &e : c->ev) (void)hipEventCreate(&e);
     c->slots_per_cu = 16;
+    c->variant = ccdk_period_in_lds() ? 1 : 4;
     if (const char *v = std::getenv("CCDGPU_KERNEL")) c->variant = (std::strcmp(v, "w1") == 0) ? 1 : 4;
     if (const char *v = std::getenv("CCDGPU_SLOTS_PER_CU")) c->slots_per_cu = std::max(1, std::atoi(v));
     *out = c;
@@ -276,9 +275,14 @@ int ccdgpu_stage(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_chips, in
         (rc = c->mask.ensure((size_t)c->total_pix * c->mask_words)) || (rc = c->counters.ensure(8)) ||
         (rc = c->stats.ensure(32)) || (rc = c->args.ensure(1)))
         return rc;
-    c->n_slots = (int32_t)std::min<int64_t>(c->total_pix, (int64_t)c->n_cu * c->slots_per_cu);
+    // persistent grid: one wave slot per resident wave (LDS / register occupancy), capped by
+    // CCDGPU_SLOTS_PER_CU
+    const int occ = ccdk_occupancy(c->variant, n_obs);
+    if (occ <= 0) return fail(CCDGPU_EHIP, "detection kernel cannot be resident with " + std::to_string(ccdk_lds_bytes(n_obs)) + " B of LDS");
+    c->n_slots = (int32_t)std::min<int64_t>(c->total_pix, (int64_t)c->n_cu * std::min(occ, c->slots_per_cu));
     const size_t ns = (size_t)c->n_slots;
-    if ((rc = c->s_date.ensure(ns * no)) || (rc = c->s_idx.ensure(ns * no)) || (rc = c->s_val.ensure(ns * 7 * no)) ||
+    const size_t nper = ccdk_period_in_lds() ? 1 : ns * no;  // global period scratch only when not in LDS
+    if ((rc = c->s_date.ensure(nper)) || (rc = c->s_row.ensure(nper * 8)) ||
         (rc = c->s_f64.ensure(ns * 8 * no)))
         return rc;
     if (c->pool_cap < c->total_pix * 8) c->pool_cap = c->total_pix * 8;
@@ -312,8 +316,7 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
     a.basis = c->basis.p;
     a.counters = c->counters.p;
     a.s_date = c->s_date.p;
-    a.s_idx = c->s_idx.p;
-    a.s_val = c->s_val.p;
+    a.s_row = c->s_row.p;
     a.s_f64 = c->s_f64.p;
     a.mask_bits = c->mask.p;
     a.procedure = c->procedure.p;
@@ -336,7 +339,7 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         if (ccdk_prep(c->dates.p, c->n_chips, c->n_obs, p.avg_days_yr, c->order.p, c->sdates.p, c->basis.p, c->stream))
             return fail(CCDGPU_EHIP, std::string("prep launch: ") + hipGetErrorString(hipGetLastError()));
         HIPCHK(hipEventRecord(c->ev[1], c->stream));
-        if (ccdk_detect(c->n_slots, c->variant, c->stream))
+        if (ccdk_detect(c->n_slots, c->variant, c->n_obs, c->stream))
             return fail(CCDGPU_EHIP, std::string("detect launch: ") + hipGetErrorString(hipGetLastError()));
         HIPCHK(hipEventRecord(c->ev[2], c->stream));
         unsigned long long h[8];
