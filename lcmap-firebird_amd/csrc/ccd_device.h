@@ -39,7 +39,8 @@ struct CcdDetectArgs {
     // per-slot scratch
     int32_t *s_date;
     uint16_t *s_row;  // [n_slots][n_obs][8]: int16 band values 0..6, uint16 sorted index
-    double *s_f64;   // [n_slots][8][n_obs] Tmask scratch / peek residuals
+    double *s_f64;   // [n_slots][8][n_obs] Tmask scratch / closest-DOY squared residuals
+    uint16_t *s_bk;  // [n_slots][n_obs] closest-DOY bucket list
     // outputs
     uint32_t *mask_bits;
     int32_t *procedure;

@@ -93,7 +93,8 @@ struct Px {
     int32_t *cd;  // compacted dates
     CRow *cr;     // compacted rows: 7 band values + sorted index, one 16-byte load per observation
 #endif
-    GLOBAL_AS double *fs;  // per-slot double scratch [8][n]
+    GLOBAL_AS double *fs;  // per-slot double scratch [8][n]: Tmask columns / closest-DOY r^2 [n][8]
+    GLOBAL_AS uint16_t *bk;  // per-slot closest-DOY bucket list [n]
     int64_t gpix;
     int nseg;
     unsigned long long fits, sweeps;
@@ -193,8 +194,14 @@ __device__ __forceinline__ int wscan_incl(int v) {
     v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
     v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);
     v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);
+    // row_bcast with a full row mask, rows selected by lane id: a partial row_mask leaves the
+    // disabled rows' destination unwritten, and the compiler's choice of "old" register for
+    // them is not reliably zero (observed wrong scans on gfx950).
+    const int row = (int)__lane_id() >> 4;
+    const int t15 = __builtin_amdgcn_update_dpp(0, v, 0x142, 0xF, 0xF, false);
+    v += (row & 1) ? t15 : 0;
+    const int t31 = __builtin_amdgcn_update_dpp(0, v, 0x143, 0xF, 0xF, false);
+    v += (row & 2) ? t31 : 0;
     return v;
 }
 // value of v in a (wave-uniform) lane, as a scalar
@@ -1186,11 +1193,22 @@ __device__ __forceinline__ void lookback(Px &P, int &wa, int &wb, int prev) {
 // find_closest_doy(period, ref, fit_window, 24) -> comparison rmse sqrt(sum r^2) / 4 per band
 // into L->comp.  The key |round(d / 365.25) * 365.25 - d| of d = t - t_ref is exactly
 // min(r, 1461 - r) / 4 with r = (4 t - 4 t_ref) mod 1461 (verified over all |d| <= 20000), so with
-// u = 4 t mod 1461 the fit window is histogrammed once per refit (L->hist2) and the 24th-smallest
-// key is found by scanning bins outward from u_ref.  Selection = keys below the threshold plus the
-// lowest-index ones at the threshold (stable argsort order, the documented tie rule).
+// u = 4 t mod 1461 the 24 closest observations are the bins within distance K of u_ref plus the
+// lowest-index ones of the two bins at distance exactly K (stable argsort order, the documented
+// tie rule).
+//
+// The fit window and the model only change at a refit, so once per (fit window, model) the window
+// is counting-sorted by u into a bucket list (P.bk, fit-relative indices; L->hist2 keeps the bin
+// end positions) and every observation's squared residuals are stored in bucket order
+// (P.fs[pos * 8 + band]).  A lookforward step then needs no pass over the window: the bins closer
+// than K are one circular run of bucket positions, read with one coalesced load per band.
 __device__ __forceinline__ int u1461(int t) { return (4 * t) % 1461; }
-__device__ __forceinline__ int hbin(const Lds *L, int u) { return (int)((L->hist2[u >> 1] >> ((u & 1) * 16)) & 0xFFFFu); }
+// L->hist2 holds two u16 per word: plain counts (closest_doy_scan) or, after build_closest, the
+// end position of each bin in the bucket list.
+__device__ __forceinline__ int h16(const Lds *L, int u) { return (int)((L->hist2[u >> 1] >> ((u & 1) * 16)) & 0xFFFFu); }
+__device__ __forceinline__ int bend(const Lds *L, int u) { return h16(L, u); }
+__device__ __forceinline__ int bstart(const Lds *L, int u) { return u == 0 ? 0 : h16(L, u - 1); }
+__device__ __forceinline__ int bcount(const Lds *L, int u) { return bend(L, u) - bstart(L, u); }
 
 __device__ __forceinline__ void build_hist(const Px &P, int fa, int fb) {
     Lds *L = &LDS();
@@ -1204,22 +1222,76 @@ __device__ __forceinline__ void build_hist(const Px &P, int fa, int fb) {
     wsync();
 }
 
-__device__ __forceinline__ void closest_doy_comp(Px &P, int fa, int fb, int ref_idx) {
+// Counting sort of the fit window [fa, fb) by u into P.bk and the squared residuals of the
+// current models (L->coef) in bucket order into P.fs.
+__device__ __forceinline__ void build_closest(const Px &P, int fa, int fb) {
+    Lds *L = &LDS();
+    const int l = lane();
+    const int nf = fb - fa;
+    build_hist(P, fa, fb);
+    // exclusive prefix over the 1461 bins: lane l owns words [12 l, 12 l + 12) (24 bins)
+    int tot = 0;
+    for (int w = 12 * l; w < 12 * l + 12 && w < 732; ++w) tot += (int)(L->hist2[w] & 0xFFFFu) + (int)(L->hist2[w] >> 16);
+    int run = wscan_incl(tot) - tot;
+    for (int w = 12 * l; w < 12 * l + 12 && w < 732; ++w) {
+        const unsigned v = L->hist2[w];
+        const int s0 = run;
+        const int s1 = run + (int)(v & 0xFFFFu);
+        run = s1 + (int)(v >> 16);
+        L->hist2[w] = (unsigned)s0 | ((unsigned)s1 << 16);  // bin start positions
+    }
+    wsync();
+    // fill: each add advances the bin's cursor, so afterwards every bin holds its end position
+    for (int i = fa + l; i < fb; i += W) {
+        const int u = u1461(CDR(P, i));
+        const unsigned old = atomicAdd(&L->hist2[u >> 1], 1u << ((u & 1) * 16));
+        const int pos = (int)((old >> ((u & 1) * 16)) & 0xFFFFu);
+        P.bk[gidx(P, pos, P.n, __LINE__)] = (uint16_t)(i - fa);
+    }
+    gsync();
+    // squared residuals in bucket order: lane = bucket position, all 7 bands per lane
+    const Lds *Lc = L;
+    for (int t0 = 0; t0 < nf; t0 += W) {
+        const int t = t0 + l;
+        if (t < nf) {
+            const int j = fa + (int)P.bk[t];
+            const int g = gidx(P, j, P.m, __LINE__);
+            const uint4 q = reinterpret_cast<const uint4 *>(PCR(P))[g];
+            const GLOBAL_AS double *bs = P.basis + (size_t)gidx(P, (int)(q.w >> 16), P.n, __LINE__) * CCD_BASIS_STRIDE;
+            double x[7];
+#pragma unroll
+            for (int c = 0; c < 7; ++c) x[c] = bs[c];
+            const unsigned qw[4] = {q.x, q.y, q.z, q.w};
+            GLOBAL_AS double *o = P.fs + (size_t)t * 8;
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                const double *c = Lc->coef[b];
+                double pr = x[0] * c[0];
+#pragma unroll
+                for (int jj = 1; jj < 7; ++jj) pr += x[jj] * c[jj];
+                pr += c[7];
+                const double y = (double)(int16_t)(qw[b >> 1] >> ((b & 1) * 16));
+                const double r = y - pr;
+                o[b] = r * r;
+            }
+        }
+    }
+    gsync();
+}
+
+__device__ __forceinline__ void closest_doy_scan(Px &P, int fa, int fb, int ref_idx) {
     Lds *L = &LDS();
     const int l = lane();
     const int nf = fb - fa;
     const int ur = u1461(CDR(P, ref_idx));
     int K = 1 << 20, need = 0;
-    PH_COUNT(P, 16, 1)
-    PH_COUNT(P, 17, nf)
-    PH_BEGIN(ts)
     if (nf > 24) {
         int carry = 0;
         for (int base = 0; base <= 730; base += W) {
             const int dd = base + l;
             int c = 0;
-            if (dd == 0) c = hbin(L, ur);
-            else if (dd <= 730) c = hbin(L, (ur + dd) % 1461) + hbin(L, (ur - dd + 1461) % 1461);
+            if (dd == 0) c = bcount(L, ur);
+            else if (dd <= 730) c = bcount(L, (ur + dd) % 1461) + bcount(L, (ur - dd + 1461) % 1461);
             const int cum = wscan_incl(c) + carry;
             const unsigned long long hit = bal(cum >= 24);
             if (hit) {
@@ -1231,8 +1303,6 @@ __device__ __forceinline__ void closest_doy_comp(Px &P, int fa, int fb, int ref_
             carry = rdl(cum, W - 1);
         }
     }
-    PH_END(P, ts, 13)
-    PH_BEGIN(ss)
     int taken_eq = 0, nsel = 0;
     for (int t0 = 0; t0 < nf; t0 += W) {
         const int i = t0 + l;
@@ -1250,8 +1320,6 @@ __device__ __forceinline__ void closest_doy_comp(Px &P, int fa, int fb, int ref_
         nsel += popc(sm);
     }
     wsync();
-    PH_END(P, ss, 14)
-    PH_BEGIN(rg)
     const int bnd = l >> 3, osub = l & 7;  // band-major: a band's 8 partial sums share a DPP row
     // nsel <= 24: three fixed rounds of 8 observations, unrolled so the row / basis gathers of
     // all three are in flight together
@@ -1267,8 +1335,102 @@ __device__ __forceinline__ void closest_doy_comp(Px &P, int fa, int fb, int ref_
     ss = gsum8(ss);
     if (osub == 0 && bnd < NB) L->comp[bnd] = sqrt(ss) / 4.0;
     wsync();
-    PH_END(P, rg, 15)
+}
+
+
+__device__ __forceinline__ void closest_doy_comp(Px &P, int fa, int fb, int ref_idx) {
+    Lds *L = &LDS();
+    const int l = lane();
+    const int nf = fb - fa;
+    PH_COUNT(P, 16, 1)
+    PH_COUNT(P, 17, nf)
     P.fl += (unsigned long long)nf * 6 + 5 * 48;  // closest-DOY keys 6 n_fit + comparison rmse 5 * 48
+    if (nf <= 24) {  // every observation of the window (no buckets built)
+        closest_doy_scan(P, fa, fb, ref_idx);
+        return;
+    }
+    const int ur = u1461(CDR(P, ref_idx));
+    PH_BEGIN(ts)
+    int K = 0, less = 0;
+    {
+        int carry = 0;
+        for (int base = 0; base <= 730; base += W) {
+            const int dd = base + l;
+            int c = 0;
+            if (dd == 0) c = bcount(L, ur);
+            else if (dd <= 730) c = bcount(L, (ur + dd) % 1461) + bcount(L, (ur - dd + 1461) % 1461);
+            const int cum = wscan_incl(c) + carry;
+            const unsigned long long hit = bal(cum >= 24);
+            if (hit) {
+                const int src = __ffsll((long long)hit) - 1;
+                K = base + src;
+                less = rdl(cum, src) - rdl(c, src);
+                break;
+            }
+            carry = rdl(cum, W - 1);
+        }
+    }
+    const int need = 24 - less;
+    // tie bins (distance exactly K): the `need` lowest fit-relative indices among their entries
+    const int b1 = (ur - K + 1461) % 1461, b2 = (ur + K) % 1461;
+    const int c1 = bcount(L, b1), c2 = (K == 0) ? 0 : bcount(L, b2);
+    const int T = c1 + c2;
+    PH_END(P, ts, 13)
+    if (T > W) {  // cannot happen for series shorter than 64 x 4 years; exact fallback
+        closest_doy_scan(P, fa, fb, ref_idx);
+        return;
+    }
+    PH_BEGIN(ss)
+    int tpos = 0, tidx = 1 << 30;
+    if (l < T) {
+        tpos = (l < c1) ? bstart(L, b1) + l : bstart(L, b2) + (l - c1);
+        tidx = (int)P.bk[gidx(P, tpos, P.n, __LINE__)];
+    }
+    int rank = 0;
+    for (int t = 0; t < T; ++t) rank += (rdl(tidx, t) < tidx) ? 1 : 0;
+    if (l < T && rank < need) L->sel[rank] = tpos;
+    wsync();
+    PH_END(P, ss, 14)
+    PH_BEGIN(rg)
+    // bins closer than K: `less` consecutive bucket positions from the start of bin u_ref - K + 1,
+    // circular over the list
+    const int s0 = (K == 0) ? 0 : bstart(L, (ur - K + 1 + 1461) % 1461);
+    const int bnd = l >> 3, osub = l & 7;  // band-major: a band's 8 partial sums share a DPP row
+    double e[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const int s2 = osub + 8 * r;
+        int pos = s0 + s2;
+        pos = pos >= nf ? pos - nf : pos;
+        if (s2 >= less) pos = L->sel[s2 - less < 24 ? s2 - less : 0];
+        e[r] = (bnd < NB) ? P.fs[(size_t)gidx(P, pos, nf, __LINE__) * 8 + bnd] : 0.0;
+    }
+    double ss = e[0];
+    ss += e[1];
+    ss += e[2];
+    ss = gsum8(ss);
+    if (osub == 0 && bnd < NB) L->comp[bnd] = sqrt(ss) / 4.0;
+    wsync();
+    PH_END(P, rg, 15)
+#ifdef CCD_CHECK_CLOSEST
+    {
+        const double mine = (l < NB) ? L->comp[l] : 0.0;
+        wsync();
+        closest_doy_scan(P, fa, fb, ref_idx);
+        const double ref = (l < NB) ? L->comp[l] : 0.0;
+        const bool bad = l < NB && fabs(mine - ref) > 1e-9 * fabs(ref);
+        if (bal(bad) && l == 0) {
+            if (atomicCAS(&c_args.stats[28], 0ull, 1ull + (unsigned long long)nf) == 0ull) {
+                c_args.stats[29] = (unsigned long long)K | ((unsigned long long)less << 16) | ((unsigned long long)T << 32);
+                c_args.stats[30] = (unsigned long long)__double_as_longlong(mine);
+                c_args.stats[31] = (unsigned long long)__double_as_longlong(ref);
+            }
+        }
+        wsync();
+        if (l < NB) L->comp[l] = mine;
+        wsync();
+    }
+#endif
 }
 
 __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
@@ -1302,7 +1464,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
             PH_BEGIN(cl)
             if (fb - fa > 24 && (hfa != fa || hfb != fb)) {
                 PH_BEGIN(hb)
-                build_hist(P, fa, fb);
+                build_closest(P, fa, fb);
                 PH_END(P, hb, 12)
                 hfa = fa;
                 hfb = fb;
@@ -1479,6 +1641,7 @@ __device__ __forceinline__ void detect_body() {
     P.cr = reinterpret_cast<CRow *>(A.s_row) + (size_t)slot * A.n_obs;
 #endif
     P.fs = as_global(A.s_f64 + (size_t)slot * 8 * A.n_obs);
+    P.bk = as_global(A.s_bk + (size_t)slot * A.n_obs);
     P.fits = 0;
     P.sweeps = 0;
     P.bad = 0;

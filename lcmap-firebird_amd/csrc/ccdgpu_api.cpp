@@ -97,6 +97,7 @@ struct ccdgpu_ctx {
     DevBuf<unsigned long long> counters, stats;
     DevBuf<int32_t> s_date;
     DevBuf<uint16_t> s_row;
+    DevBuf<uint16_t> s_bk;
     DevBuf<uint32_t> mask;
     DevBuf<ccdgpu_segment> pool, csr;
     DevBuf<CcdDetectArgs> args;
@@ -113,6 +114,7 @@ struct ccdgpu_ctx {
         counters.release();
         stats.release();
         s_row.release();
+        s_bk.release();
         mask.release();
         pool.release();
         csr.release();
@@ -283,7 +285,7 @@ int ccdgpu_stage(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_chips, in
     const size_t ns = (size_t)c->n_slots;
     const size_t nper = ccdk_period_in_lds() ? 1 : ns * no;  // global period scratch only when not in LDS
     if ((rc = c->s_date.ensure(nper)) || (rc = c->s_row.ensure(nper * 8)) ||
-        (rc = c->s_f64.ensure(ns * 8 * no)))
+        (rc = c->s_f64.ensure(ns * 8 * no)) || (rc = c->s_bk.ensure(ns * no)))
         return rc;
     if (c->pool_cap < c->total_pix * 8) c->pool_cap = c->total_pix * 8;
     if ((rc = c->pool.ensure(c->pool_cap)) || (rc = c->pool_seq.ensure(c->pool_cap))) return rc;
@@ -317,6 +319,7 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
     a.counters = c->counters.p;
     a.s_date = c->s_date.p;
     a.s_row = c->s_row.p;
+    a.s_bk = c->s_bk.p;
     a.s_f64 = c->s_f64.p;
     a.mask_bits = c->mask.p;
     a.procedure = c->procedure.p;
