@@ -73,6 +73,11 @@ struct __attribute__((aligned(16))) Lds {
 __constant__ CcdDetectArgs c_args;
 extern __shared__ __attribute__((aligned(16))) char ccd_smem[];
 __device__ __forceinline__ Lds &LDS() { return *reinterpret_cast<Lds *>(ccd_smem); }
+// Peek-residual ring, band-major [band][64 observations], in the row staging tile (the Gram
+// staging never overlaps a live ring): lane-contiguous, so lane-per-observation access is
+// bank-conflict free.
+__device__ __forceinline__ double *PRES(Lds *L) { return &L->row[0][0]; }
+static_assert(TR * RW >= 8 * CCD_WAVE, "row tile holds the 8 x 64 residual ring");
 
 // One compacted observation: the 7 band values and its sorted-date index in one 16-byte row, so a
 // random gather (closest-DOY, peek) touches one cache line instead of eight.
@@ -1121,7 +1126,7 @@ __device__ __forceinline__ bool eval_peek(Px &P, int k, int start, int dir, doub
         double r = 0.0;
         if (pass < 4) r = rr[pass < 4 ? pass : 0];
         else if (valid) r = resid_at(P, bnd, start + dir * jj);
-        if (jj < k) (&L->row[0][0])[jj * 8 + bnd] = r;  // kept for the segment's magnitude medians
+        if (jj < k && bnd < NB) PRES(L)[bnd * W + jj] = r;  // kept for the segment's magnitude medians
         const double v = r / rm;
         const double mag = gsum8((valid && det) ? v * v : 0.0);
         if (bal(bnd == 0 && jj < k && !(mag > P.chg))) all = false;
@@ -1133,19 +1138,21 @@ __device__ __forceinline__ bool eval_peek(Px &P, int k, int start, int dir, doub
     return all;
 }
 
-// Median over the k peek residuals of each band (lookforward result magnitudes, taken from
-// the LDS row buffer where eval_peek left them); returns band l's median in lane l (l < 7).
-__device__ __forceinline__ double peek_medians(Px &P, int k) {
+// Median over the k peek residuals of each band of the window whose residuals start at ring
+// offset off (band-major ring PRES, written by eval_peek or ring_rows); returns band l's median in
+// lane l (l < 7).
+__device__ __forceinline__ double peek_medians(Px &P, int k, int off) {
     Lds *L = &LDS();
     const int l = lane();
     const int bnd = l & 7, osub = l >> 3;
     const int t1 = (k - 1) / 2, t2 = k / 2;
+    const double *R = PRES(L) + bnd * W + off;
     for (int jj = osub; jj < k; jj += 8) {
         if (bnd >= NB) continue;
-        const double v = (&L->row[0][0])[jj * 8 + bnd];
+        const double v = R[jj];
         int rank = 0;
         for (int i = 0; i < k; ++i) {
-            const double u = (&L->row[0][0])[i * 8 + bnd];
+            const double u = R[i];
             rank += (u < v || (u == v && i < jj)) ? 1 : 0;
         }
         if (rank == t1) L->med1[bnd] = v;
@@ -1338,104 +1345,109 @@ __device__ __forceinline__ void closest_doy_scan(Px &P, int fa, int fb, int ref_
 }
 
 
-__device__ __forceinline__ void closest_doy_comp(Px &P, int fa, int fb, int ref_idx) {
+// Residuals of the current models at compacted positions x0 .. x0 + 63 (lane = position) into
+// the band-major ring PRES (same arithmetic as resid_at).
+__device__ __forceinline__ void ring_rows(const Px &P, int x0) {
     Lds *L = &LDS();
     const int l = lane();
-    const int nf = fb - fa;
-    PH_COUNT(P, 16, 1)
-    PH_COUNT(P, 17, nf)
-    P.fl += (unsigned long long)nf * 6 + 5 * 48;  // closest-DOY keys 6 n_fit + comparison rmse 5 * 48
-    if (nf <= 24) {  // every observation of the window (no buckets built)
-        closest_doy_scan(P, fa, fb, ref_idx);
-        return;
-    }
-    const int ur = u1461(CDR(P, ref_idx));
-    PH_BEGIN(ts)
-    int K = 0, less = 0;
-    {
-        int carry = 0;
-        for (int base = 0; base <= 730; base += W) {
-            const int dd = base + l;
-            int c = 0;
-            if (dd == 0) c = bcount(L, ur);
-            else if (dd <= 730) c = bcount(L, (ur + dd) % 1461) + bcount(L, (ur - dd + 1461) % 1461);
-            const int cum = wscan_incl(c) + carry;
-            const unsigned long long hit = bal(cum >= 24);
-            if (hit) {
-                const int src = __ffsll((long long)hit) - 1;
-                K = base + src;
-                less = rdl(cum, src) - rdl(c, src);
-                break;
-            }
-            carry = rdl(cum, W - 1);
-        }
-    }
-    const int need = 24 - less;
-    // tie bins (distance exactly K): the `need` lowest fit-relative indices among their entries
-    const int b1 = (ur - K + 1461) % 1461, b2 = (ur + K) % 1461;
-    const int c1 = bcount(L, b1), c2 = (K == 0) ? 0 : bcount(L, b2);
-    const int T = c1 + c2;
-    PH_END(P, ts, 13)
-    if (T > W) {  // cannot happen for series shorter than 64 x 4 years; exact fallback
-        closest_doy_scan(P, fa, fb, ref_idx);
-        return;
-    }
-    PH_BEGIN(ss)
-    int tpos = 0, tidx = 1 << 30;
-    if (l < T) {
-        tpos = (l < c1) ? bstart(L, b1) + l : bstart(L, b2) + (l - c1);
-        tidx = (int)P.bk[gidx(P, tpos, P.n, __LINE__)];
-    }
-    int rank = 0;
-    for (int t = 0; t < T; ++t) rank += (rdl(tidx, t) < tidx) ? 1 : 0;
-    if (l < T && rank < need) L->sel[rank] = tpos;
-    wsync();
-    PH_END(P, ss, 14)
-    PH_BEGIN(rg)
-    // bins closer than K: `less` consecutive bucket positions from the start of bin u_ref - K + 1,
-    // circular over the list
-    const int s0 = (K == 0) ? 0 : bstart(L, (ur - K + 1 + 1461) % 1461);
-    const int bnd = l >> 3, osub = l & 7;  // band-major: a band's 8 partial sums share a DPP row
-    double e[3];
+    const int j = x0 + l;
+    double *R = PRES(L) + l;
+    if (j < P.m) {
+        const CRow cw = CROW(P, j);
+        const GLOBAL_AS double *bs = P.basis + (size_t)cw.ci * CCD_BASIS_STRIDE;
+        double x[7];
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {
-        const int s2 = osub + 8 * r;
-        int pos = s0 + s2;
-        pos = pos >= nf ? pos - nf : pos;
-        if (s2 >= less) pos = L->sel[s2 - less < 24 ? s2 - less : 0];
-        e[r] = (bnd < NB) ? P.fs[(size_t)gidx(P, pos, nf, __LINE__) * 8 + bnd] : 0.0;
-    }
-    double ss = e[0];
-    ss += e[1];
-    ss += e[2];
-    ss = gsum8(ss);
-    if (osub == 0 && bnd < NB) L->comp[bnd] = sqrt(ss) / 4.0;
-    wsync();
-    PH_END(P, rg, 15)
-#ifdef CCD_CHECK_CLOSEST
-    {
-        const double mine = (l < NB) ? L->comp[l] : 0.0;
-        wsync();
-        closest_doy_scan(P, fa, fb, ref_idx);
-        const double ref = (l < NB) ? L->comp[l] : 0.0;
-        const bool bad = l < NB && fabs(mine - ref) > 1e-9 * fabs(ref);
-        if (bal(bad) && l == 0) {
-            if (atomicCAS(&c_args.stats[28], 0ull, 1ull + (unsigned long long)nf) == 0ull) {
-                c_args.stats[29] = (unsigned long long)K | ((unsigned long long)less << 16) | ((unsigned long long)T << 32);
-                c_args.stats[30] = (unsigned long long)__double_as_longlong(mine);
-                c_args.stats[31] = (unsigned long long)__double_as_longlong(ref);
-            }
+        for (int c = 0; c < 7; ++c) x[c] = bs[c];
+#pragma unroll
+        for (int bd = 0; bd < NB; ++bd) {
+            const double *c = L->coef[bd];
+            double pr = x[0] * c[0];
+#pragma unroll
+            for (int jj = 1; jj < 7; ++jj) pr += x[jj] * c[jj];
+            pr += c[7];
+            R[bd * W] = (double)cw.v[bd] - pr;
         }
-        wsync();
-        if (l < NB) L->comp[l] = mine;
-        wsync();
     }
-#endif
+    wsync();
 }
 
+// Entries of the fit window whose closest-DOY bin lies within circular distance d of bin u
+// (L->hist2 = bin end positions after build_closest).
+__device__ __forceinline__ int cnt_within(const Lds *L, int nf, int u, int d) {
+    if (d >= 730) return nf;
+    const int lo = u - d, hi = u + d;
+    if (lo >= 0 && hi <= 1460) return bend(L, hi) - (lo > 0 ? bend(L, lo - 1) : 0);
+    if (lo < 0) return bend(L, hi) + nf - bend(L, lo + 1460);
+    return nf - (lo > 0 ? bend(L, lo - 1) : 0) + bend(L, hi - 1461);
+}
+
+// Per-lane find_closest_doy(period, ref, fit_window, 24) comparison rmse (change.lookforward):
+// the 24 fit-window observations closest in day of year to date dref, sqrt(sum r^2) / 4 per band,
+// from the bucket list and bucket-ordered squared residuals build_closest left (nf > 24).
+// Entries at distance < K form one circular run of bucket positions; at distance exactly K the
+// lowest fit-relative indices win (stable argsort).
+__device__ __forceinline__ void comp_lane(const Px &P, int nf, int dref, double (&cs)[NB]) {
+    const Lds *L = &LDS();
+    const int u = u1461(dref);
+    int lo = 0, hi = 730;  // smallest K with cnt_within(K) >= 24
+#pragma unroll
+    for (int it = 0; it < 10; ++it) {
+        if (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (cnt_within(L, nf, u, mid) >= 24) hi = mid;
+            else lo = mid + 1;
+        }
+    }
+    const int K = lo;
+    const int less = K > 0 ? cnt_within(L, nf, u, K - 1) : 0;
+    const int need = 24 - less;
+#pragma unroll
+    for (int bd = 0; bd < NB; ++bd) cs[bd] = 0.0;
+    const int s0 = K > 0 ? bstart(L, (u - K + 1 + 1461) % 1461) : 0;
+    for (int s = 0; s < less; ++s) {
+        int pos = s0 + s;
+        pos = pos >= nf ? pos - nf : pos;
+        const GLOBAL_AS double *f = P.fs + (size_t)gidx(P, pos, nf, __LINE__) * 8;
+#pragma unroll
+        for (int bd = 0; bd < NB; ++bd) cs[bd] += f[bd];
+    }
+    const int b1 = (u - K + 1461) % 1461, b2 = (u + K) % 1461;
+    const int c1 = bcount(L, b1), c2 = K > 0 ? bcount(L, b2) : 0;
+    const int st1 = bstart(L, b1), st2 = bstart(L, b2);
+    const int T = c1 + c2;
+    for (int e = 0; e < T; ++e) {
+        const int pe = e < c1 ? st1 + e : st2 + (e - c1);
+        const int ie = (int)P.bk[gidx(P, pe, P.n, __LINE__)];
+        int rank = 0;
+        for (int f2 = 0; f2 < T; ++f2) {
+            const int pf = f2 < c1 ? st1 + f2 : st2 + (f2 - c1);
+            rank += ((int)P.bk[gidx(P, pf, P.n, __LINE__)] < ie) ? 1 : 0;
+        }
+        if (rank < need) {
+            const GLOBAL_AS double *f = P.fs + (size_t)gidx(P, pe, nf, __LINE__) * 8;
+#pragma unroll
+            for (int bd = 0; bd < NB; ++bd) cs[bd] += f[bd];
+        }
+    }
+#pragma unroll
+    for (int bd = 0; bd < NB; ++bd) cs[bd] = sqrt(cs[bd]) / 4.0;
+}
+
+// change.lookforward.  The first steps (no model yet, or fewer than 24 observations in the
+// window) refit every step and run one at a time.  After that the model changes only at a refit
+// (window span >= 1.33 x the fitted span), so the steps between refits are evaluated in batches,
+// lane = step: a step at window start x uses the peek observations x .. x + k - 1 and the
+// reference date of x + k - 1.  Only the first peek observation can be removed (outlier), so in
+// the batch's own indexing every step's window is consecutive and the step sequence is fixed:
+// step x removes x (outlier) or advances past it, and the batch ends at the first step that
+// needs a refit (span test on the last kept observation before it) or detects a change.
+// Removals are applied in one compaction pass per batch.
 __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
     const ccdgpu_params &p = c_args.p;
+    Lds *L = &LDS();
     const int l = lane();
+    const int k = P.peek;
+    const int B = W - (k - 1);  // steps per batch: windows x .. x + k - 1 stay inside the 64-row ring
     int a = wa, b = wb;
     int fa = a, fb = b;
     bool have = false;
@@ -1443,54 +1455,134 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
     int nc = p.coef_min;
     double fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
     int peek_start = b;
-    int hfa = -1, hfb = -1;  // fit window the closest-DOY histogram describes
-    while (b + P.peek < P.m || !have) {
-        nc = num_coefs(p, b - a);
-        peek_start = b;
-        const int k = P.peek;
-        const double model_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
-        const bool early = !have || b - a < 24;  // refit every step, comparison rmse = model rmse
-        if (early || model_span >= 1.33 * fit_span) {
+    int moff = 0;            // ring offset of the last evaluated peek window
+    int hfa = -1, hfb = -1;  // fit window the closest-DOY buckets describe
+    for (;;) {
+        if (!(b + k < P.m || !have)) break;
+        if (!have || b - a < 24) {
+            // early step: refit every step, comparison rmse = model rmse
+            nc = num_coefs(p, b - a);
+            peek_start = b;
             fa = a;
             fb = b;
             fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
             fit_models(P, fa, fb, nc);
             have = true;
-        }
-        if (early) {
-            if (l < NB) LDS().comp[l] = LDS().rmse[l];
+            if (l < NB) L->comp[l] = L->rmse[l];
             wsync();
-        } else {
-            PH_BEGIN(cl)
-            if (fb - fa > 24 && (hfa != fa || hfb != fb)) {
-                PH_BEGIN(hb)
-                build_closest(P, fa, fb);
-                PH_END(P, hb, 12)
-                hfa = fa;
-                hfb = fb;
+            double m0;
+            PH_BEGIN(ep)
+            const bool chg_now = eval_peek(P, k, b, 1, m0);
+            PH_END(P, ep, 8)
+            moff = 0;
+            if (chg_now) {
+                change = 1.0;
+                break;
             }
-            closest_doy_comp(P, fa, fb, b + k - 1);
-            PH_END(P, cl, 7)
+            if (m0 > p.outlier_threshold) {
+                const int rm = b;
+                compact_drop(P, rm, [&](int j) { return j == rm; });
+                continue;
+            }
+            b += 1;
+            continue;
         }
-        double m0;
-        PH_BEGIN(ep)
-        const bool chg_now = eval_peek(P, k, b, 1, m0);
-        PH_END(P, ep, 8)
-        if (chg_now) {
+        // ---- batch of up to B steps at window starts x0 .. x0 + B - 1 (model fixed)
+        const int nf = fb - fa;
+        if (nf > 24 && (hfa != fa || hfb != fb)) {
+            PH_BEGIN(hb)
+            build_closest(P, fa, fb);
+            PH_END(P, hb, 12)
+            hfa = fa;
+            hfb = fb;
+        }
+        if (nf <= 24) closest_doy_scan(P, fa, fb, b);  // every fit observation: one comp for all steps
+        PH_BEGIN(cl)
+        const int x0 = b, m0 = P.m;
+        ring_rows(P, x0);
+        const bool valid = l < B && x0 + l + k < m0;
+        const unsigned long long V = bal(valid);
+        const int da = CDR(P, a);
+        const int dprev = CDR(P, x0 - 1);
+        int dj = 0;
+        bool allc = false, outj = false;
+        if (valid) {
+            dj = CDR(P, x0 + l);
+            double cs[NB];
+            if (nf > 24) {
+                comp_lane(P, nf, CDR(P, x0 + l + k - 1), cs);
+            } else {
+#pragma unroll
+                for (int bd = 0; bd < NB; ++bd) cs[bd] = L->comp[bd];
+            }
+            const double *R = PRES(L) + l;
+            double rmv[NB];
+#pragma unroll
+            for (int bd = 0; bd < NB; ++bd) {
+                const double vr = L->vario[bd], cr = cs[bd];
+                rmv[bd] = (vr != vr || cr != cr) ? __builtin_nan("") : (vr > cr ? vr : cr);
+            }
+            allc = true;
+            for (int jj = 0; jj < k; ++jj) {
+                double mg = 0.0;
+#pragma unroll
+                for (int bd = 0; bd < NB; ++bd) {
+                    if ((p.detection_bands >> bd) & 1u) {
+                        const double v = R[bd * W + jj] / rmv[bd];
+                        mg += v * v;
+                    }
+                }
+                allc = allc && (mg > P.chg);
+                if (jj == 0) outj = mg > p.outlier_threshold;
+            }
+        }
+        const unsigned long long O = bal(valid && outj);
+        const unsigned long long lower = (V & ~O) & ((1ull << l) - 1ull);
+        const int lk = lower ? 63 - __clzll(lower) : 0;
+        const int dsh = __shfl(dj, lk);
+        const int dlk = lower ? dsh : dprev;  // date at position b - 1 when step l starts
+        const bool trig = valid && ((double)dlk - (double)da) >= 1.33 * fit_span;
+        const unsigned long long TG = bal(trig);
+        const unsigned long long Tm = bal(valid && (trig || allc));
+        const int nv = popc(V);
+        const int xs = Tm ? __ffsll((long long)Tm) - 1 : nv;  // first step not executed as a plain step
+        const bool change_here = Tm && !((TG >> xs) & 1ull);
+        // steps executed: 0 .. xs - 1 (plus xs itself when it detects the change)
+        const int ne = change_here ? xs + 1 : xs;
+        P.fl += (unsigned long long)ne *
+                ((unsigned long long)k * (7 * 2 * 8 + 5 * 3) + (unsigned long long)nf * 6 + 5 * 48);
+        PH_COUNT(P, 16, ne)
+        PH_END(P, cl, 7)
+        const unsigned long long rem = xs >= 64 ? O : (O & ((1ull << xs) - 1ull));
+        const int R = popc(rem);
+        if (ne > 0) {
+            const int last = ne - 1;  // last executed step
+            peek_start = x0 + last - popc(rem & ((1ull << last) - 1ull));
+            nc = num_coefs(p, peek_start - a);
+            moff = last;
+        }
+        if (R) {
+            PH_BEGIN(cp)
+            compact_drop(P, x0, [&](int j) { return j - x0 < 64 && ((rem >> (j - x0)) & 1ull); });
+            PH_END(P, cp, 9)
+        }
+        if (change_here) {
+            b = peek_start;
             change = 1.0;
             break;
         }
-        if (m0 > p.outlier_threshold) {
-            const int rm = b;
-            PH_BEGIN(cp)
-            compact_drop(P, rm, [&](int j) { return j == rm; });
-            PH_END(P, cp, 9)
-            continue;
+        b = x0 + xs - R;
+        if (Tm) {
+            // refit at step xs (its evaluation runs in the next batch with the new model)
+            nc = num_coefs(p, b - a);
+            fa = a;
+            fb = b;
+            fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
+            fit_models(P, fa, fb, nc);
         }
-        b += 1;
     }
     PH_BEGIN(md)
-    const double mag_lane = peek_medians(P, P.peek);
+    const double mag_lane = peek_medians(P, k, moff);
     emit(P, CDR(P, a), CDR(P, b - 1), CDR(P, peek_start), b - a, change, nc, mag_lane);
     PH_END(P, md, 11)
     wa = a;
