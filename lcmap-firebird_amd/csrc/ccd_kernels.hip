@@ -129,13 +129,22 @@ static_assert(sizeof(Lds) % 16 == 0, "period rows follow the Lds block 16-byte a
 // ------------------------------------------------------------------ diagnostic phase timers
 // Built only into lib/libccdgpu_diag.so (-DCCD_PHASE_TIMERS): s_memtime cycle totals per phase,
 // summed over waves into stats[8 + phase].  Phases: 0 pixel total, 1 QA/filter/compaction,
-// 2 variogram + peek, 3 Tmask, 4 Lasso Gram, 5 Lasso CD, 6 Lasso rmse, 7 closest-DOY rmse,
-// 8 peek evaluation, 9 outlier compaction, 10 stability, 11 medians + emit; closest-DOY split:
-// 12 histogram build, 13 threshold scan, 14 selection scan, 15 residual gather; event counts:
-// 16 closest-DOY calls, 17 summed fit-window length, 18 peek evaluations, 19 fits.
+// 2 variogram + peek, 3 Tmask, 4 Lasso Gram, 5 Lasso CD, 6 Lasso rmse, 7 lookforward batch
+// (13 ring residuals + 14 per-lane closest-DOY rmse + 15 magnitudes + decisions), 8 single-step
+// peek evaluation, 9 outlier compaction, 10 stability, 11 medians + emit, 12 closest-DOY bucket
+// build; event counts: 16 batched steps executed, 17 batches, 18 single-step peek evaluations,
+// 19 fits.  Per-lane phases (14, 15) are summed in lane 0 only.
 #ifdef CCD_PHASE_TIMERS
-#define PH_BEGIN(id) const unsigned long long _ph_##id = __builtin_amdgcn_s_memtime();
-#define PH_END(P, id, slot) (P).tph[slot] += __builtin_amdgcn_s_memtime() - _ph_##id;
+// s_memtime returns through lgkmcnt out of order with LDS traffic: drain every counter around
+// each stamp so no LDS result can be consumed early.
+__device__ __forceinline__ unsigned long long ph_stamp() {
+    __builtin_amdgcn_s_waitcnt(0);
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_s_waitcnt(0);
+    return t;
+}
+#define PH_BEGIN(id) const unsigned long long _ph_##id = ph_stamp();
+#define PH_END(P, id, slot) (P).tph[slot] += ph_stamp() - _ph_##id;
 #define PH_COUNT(P, slot, v) (P).tph[slot] += (unsigned long long)(v);
 #else
 #define PH_COUNT(P, slot, v)
@@ -181,10 +190,12 @@ __device__ __forceinline__ int below(unsigned long long m) {
 // DPP lane moves on a double (two 32-bit halves).  Controls: 0xB1 quad_perm [1,0,3,2] (xor 1),
 // 0x4E quad_perm [2,3,0,1] (xor 2), 0x141 row_half_mirror (lane i <-> 7-i in each 8),
 // 0x140 row_mirror (lane i <-> 15-i in each 16).
+// (Every lane's source is valid for the permutations used with dpp<>, so bound_ctrl only saves
+// the compiler a zero "old" operand.)
 template <int CTRL>
 __device__ __forceinline__ double dpp(double v) {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, true);
     return __hiloint2double(hi, lo);
 }
 __device__ __forceinline__ double rdlane(double v, int l) {
@@ -382,10 +393,43 @@ __device__ __forceinline__ double gmax8(double v) {
     return t > v ? t : v;
 }
 
-// sklearn 0.18 enet_coordinate_descent (beta = 0, cyclic, duality-gap stop) in Gram form,
-// 7 bands at once: lane = band * 8 + coordinate.  Lane (b, k) holds Gram column k, q_k = Xc_k.yc_b
-// and w_k; the partial sum of coordinate j's update is an 8-lane butterfly.  Writes
-// L->coef[b][0..6]; returns the sweep count (every lane of the band's group).
+// Lane (group base + J) of every 8-lane group, broadcast to the whole group: quad_perm broadcast
+// inside each quad, then row_shr / row_shl 4 carries it to the other quad of the group.
+template <int J>
+__device__ __forceinline__ double bcast8(double v) {
+    constexpr int q = (J & 3) * 0x55;  // quad_perm [J%4, J%4, J%4, J%4]
+    const double t = dpp<q>(v);
+    const bool upper = (lane() & 4) != 0;
+    if (J < 4) {
+        const double u = dpp<0x114>(t);  // row_shr:4 -- lane i <- lane i - 4
+        return upper ? u : t;
+    } else {
+        const double u = dpp<0x104>(t);  // row_shl:4 -- lane i <- lane i + 4
+        return upper ? t : u;
+    }
+}
+
+// One coordinate of the cyclic sweep (coordinate J of every band group).  Lane (b, k) holds
+// g_k = q_k - sum_m G_km w_m (the correlation X_k . R of sklearn's residual form); coordinate J's
+// update uses tmp = X_J . (R + w_J X_J) = g_J + G_JJ w_J, then every g_k absorbs the change.
+template <int J>
+__device__ __forceinline__ void cd_coord(int k, bool live, double alpha, double gkk, double rgkk,
+                                         double gcolJ, double &g, double &w) {
+    const double tmp = g + gkk * w;
+    const double aa = fabs(tmp) - alpha;
+    const double wn = aa > 0.0 ? (tmp > 0.0 ? aa : -aa) * rgkk : 0.0;
+    const bool upd = live && k == J;
+    const double wnew = upd ? wn : w;
+    const double d = wnew - w;  // 0 outside the updated lane
+    w = wnew;
+    g -= gcolJ * bcast8<J>(d);
+}
+
+// sklearn 0.18 enet_coordinate_descent (beta = 0, cyclic, duality-gap stop) in gradient form,
+// 7 bands at once: lane = band * 8 + coordinate.  Lane (b, k) holds Gram column k, g_k and w_k;
+// a coordinate update is broadcast to its band group by DPP and folded into every g (no
+// per-coordinate reduction).  Writes L->coef[b][0..6]; returns the sweep count (every lane of
+// the band's group).
 __device__ __forceinline__ int cd_lanes(Lds *L, int pc, double alpha, int max_iter, double tol) {
     const int l = lane();
     const int b = l >> 3, k = l & 7;
@@ -398,36 +442,34 @@ __device__ __forceinline__ int cd_lanes(Lds *L, int pc, double alpha, int max_it
     const double q = act ? L->Q[k][b] : 0.0;
     const double yy = b < NB ? L->YY[b] : 0.0;
     const double tol_s = tol * yy;
-    double w = 0.0;
+    const bool can = act && gkk != 0.0;  // sklearn skips zero-norm columns
+    double w = 0.0, g = q;
     bool done = b >= NB;
     int sweeps = max_iter;
     for (int it = 0; it < max_iter; ++it) {
         if (bal(!done) == 0ull) break;
-        double dl = 0.0;
-#pragma unroll
-        for (int j = 0; j < 7; ++j) {
-            if (j >= pc) break;
-            const double s = gsum8((act && k != j) ? gcol[j] * w : 0.0);
-            if (act && !done && k == j && gkk != 0.0) {
-                const double tmp = q - s;
-                const double aa = fabs(tmp) - alpha;
-                const double wn = aa > 0.0 ? (tmp > 0.0 ? aa : -aa) * rgkk : 0.0;
-                dl = fabs(wn - w);
-                w = wn;
-            }
-        }
-        const double d_w_max = gmax8(dl);
+        const bool live = can && !done;
+        const double w0 = w;
+        cd_coord<0>(k, live, alpha, gkk, rgkk, gcol[0], g, w);
+        if (pc > 1) cd_coord<1>(k, live, alpha, gkk, rgkk, gcol[1], g, w);
+        if (pc > 2) cd_coord<2>(k, live, alpha, gkk, rgkk, gcol[2], g, w);
+        if (pc > 3) cd_coord<3>(k, live, alpha, gkk, rgkk, gcol[3], g, w);
+        if (pc > 4) cd_coord<4>(k, live, alpha, gkk, rgkk, gcol[4], g, w);
+        if (pc > 5) cd_coord<5>(k, live, alpha, gkk, rgkk, gcol[5], g, w);
+        if (pc > 6) cd_coord<6>(k, live, alpha, gkk, rgkk, gcol[6], g, w);
+        // every coordinate moves once per sweep: d_w_ii = |w_new - w_old| of the lane's own one
+        const double d_w_max = gmax8(fabs(w - w0));
         const double w_max = gmax8(act ? fabs(w) : 0.0);
-        const bool check = !done && (w_max == 0.0 || d_w_max / w_max < tol || it == max_iter - 1);
+        // d_w_max / w_max < tol, with the division only where the quotient is near tol
+        const double tw = tol * w_max;
+        const bool near = !done && w_max != 0.0 && (w_max < 1e-280 || (d_w_max > 0.25 * tw && d_w_max < 4.0 * tw));
+        bool ratio_lt = d_w_max <= 0.25 * tw;
+        if (bal(near)) {
+            if (near) ratio_lt = d_w_max / w_max < tol;
+        }
+        const bool check = !done && (w_max == 0.0 || ratio_lt || it == max_iter - 1);
         if (bal(check)) {
-            double gw = 0.0;
-#pragma unroll
-            for (int kk = 0; kk < 7; ++kk) {
-                if (kk >= pc) break;
-                const double t = gsum8(act ? gcol[kk] * w : 0.0);
-                if (k == kk) gw = t;
-            }
-            const double xta = act ? q - gw : 0.0;
+            const double xta = act ? g : 0.0;  // X^T R
             const double dual = gmax8(fabs(xta));
             const double wq = gsum8(w * q);
             const double wxta = gsum8(w * xta);
@@ -558,6 +600,7 @@ __device__ __forceinline__ void fit_models(Px &P, int a, int b, int k) {
         L->coef[l][7] = L->ym[l] - dot;
     }
     P.fits += NB;
+    PH_COUNT(P, 19, 1)
     // SURVEY.md 8(d) op-count model: Gram + column sums n k (k+1), RHS 7 * 2 n k,
     // residual / rmse 7 (2 n k + 3 n)  (k = number of coefficients incl. intercept)
     P.fl += (unsigned long long)nw * (unsigned long long)(k * (k + 1) + 14 * k + 7 * (2 * k + 3));
@@ -1499,7 +1542,10 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
         if (nf <= 24) closest_doy_scan(P, fa, fb, b);  // every fit observation: one comp for all steps
         PH_BEGIN(cl)
         const int x0 = b, m0 = P.m;
+        PH_BEGIN(rr)
         ring_rows(P, x0);
+        PH_END(P, rr, 13)
+        PH_COUNT(P, 17, 1)
         const bool valid = l < B && x0 + l + k < m0;
         const unsigned long long V = bal(valid);
         const int da = CDR(P, a);
@@ -1509,12 +1555,15 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
         if (valid) {
             dj = CDR(P, x0 + l);
             double cs[NB];
+            PH_BEGIN(cmp)
             if (nf > 24) {
                 comp_lane(P, nf, CDR(P, x0 + l + k - 1), cs);
             } else {
 #pragma unroll
                 for (int bd = 0; bd < NB; ++bd) cs[bd] = L->comp[bd];
             }
+            PH_END(P, cmp, 14)
+            PH_BEGIN(mg)
             const double *R = PRES(L) + l;
             double rmv[NB];
 #pragma unroll
@@ -1535,6 +1584,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
                 allc = allc && (mg > P.chg);
                 if (jj == 0) outj = mg > p.outlier_threshold;
             }
+            PH_END(P, mg, 15)
         }
         const unsigned long long O = bal(valid && outj);
         const unsigned long long lower = (V & ~O) & ((1ull << l) - 1ull);

@@ -17,9 +17,9 @@ ctx.stage(np.stack([d[0] for d in data]), np.stack([d[1] for d in data]), np.sta
 ctx.run()
 st, dc = ctx.stats(), ctx.diag_counters()
 names = ['pixel total', 'QA/filter/compact', 'variogram+peek', 'tmask', 'lasso gram', 'lasso cd',
-         'lasso rmse', 'closest-doy rmse', 'peek eval', 'outlier compaction', 'stability', 'medians+emit',
-         'cl: hist build', 'cl: threshold scan', 'cl: selection scan', 'cl: residual gather']
-counts = ['closest calls', 'closest nf sum', 'peek evals']
+         'lasso rmse', 'lf batch', 'single-step peek eval', 'outlier compaction', 'stability', 'medians+emit',
+         'closest bucket build', 'batch: ring residuals', 'batch: closest-doy (lane)', 'batch: magnitudes']
+counts = ['batched steps', 'batches', 'single-step peek evals', 'fit calls']
 tot = dc[8] or 1
 out = {'config': which, 'chips': chips, 'detect_ms': st['detect_ms'], 'fits': dc[0], 'sweeps': dc[1],
        'sweeps_per_fit': dc[1] / max(1, dc[0] / 7)}
