@@ -62,10 +62,16 @@ struct __attribute__((aligned(16))) Lds {
     double comp[8];        // comparison rmse per band (change_magnitude)
     double med1[8], med2[8];
     uint32_t mask[MAXW];   // processing mask, sorted order
-    uint32_t tflag[MAXW];  // Tmask outlier flags of the current window
     int sel[32];           // compacted indices of the 24 closest-DOY observations
-    double tchol[5][5];    // Tmask: Cholesky factor of the unweighted normal matrix
-    uint32_t hist2[732];   // closest-DOY: fit-window counts per (4 t mod 1461) bin, 2 x u16 per word
+    double S[98];          // raw Gram sums of the accumulated window (entry map: gram_entry)
+    int y0[8];             // per-band value shift of the accumulated window
+    union {                // Tmask (initialize) and the closest-DOY buckets (lookforward) never overlap
+        uint32_t hist2[732];   // closest-DOY: fit-window counts per (4 t mod 1461) bin, 2 x u16 per word
+        struct {
+            uint32_t tflag[MAXW];  // Tmask outlier flags of the current window
+            double tchol[5][5];    // Tmask: Cholesky factor of the unweighted normal matrix
+        };
+    };
 };
 
 // Launch arguments live in constant memory (uniform scalar loads from every device function);
@@ -102,6 +108,9 @@ struct Px {
     GLOBAL_AS uint16_t *bk;  // per-slot closest-DOY bucket list [n]
     int64_t gpix;
     int nseg;
+    int acc_a, acc_b;  // window [acc_a, acc_b) whose raw sums L->S holds (acc_a < 0: none)
+    int acc_t0;        // date shift of those sums
+    int fit_k;         // coefficients of the models in L->coef when they describe [acc_a, acc_b)
     unsigned long long fits, sweeps;
     unsigned long long fl;       // counted FP64 flops, wave-uniform part
     unsigned long long fl_lane;  // counted FP64 flops, per-lane part (coordinate descent)
@@ -336,6 +345,7 @@ template <class F>
 __device__ __forceinline__ int compact_drop(Px &P, int a, F drop) {
     const int l = lane();
     int out = a;
+    if (a < P.acc_b) P.acc_a = -1;  // rows of the accumulated Gram window may move
     for (int base = a; base < P.m; base += W) {
         const int j = base + l;
         const bool in = j < P.m;
@@ -363,17 +373,118 @@ __device__ __forceinline__ int compact_drop(Px &P, int a, F drop) {
 }
 
 // ------------------------------------------------------------------ Lasso (models/lasso.py)
+// Stage rows j0 .. j0 + cnt - 1 of the period into the LDS tile as
+// [t - t0, cos wt, sin wt, cos 2wt, sin 2wt, cos 3wt, sin 3wt, 1, y0 - s0 .. y6 - s6, 0]
+// (t0, s = the accumulated window's integer shifts: exact, and they keep the raw sums small).
 __device__ __forceinline__ void stage_rows(const Px &P, int j0, int cnt) {
+    Lds *L = &LDS();
     const int l = lane();
     if (l < cnt) {
         const int j = j0 + l;
         const CRow cw = CROW(P, j);
         const GLOBAL_AS double *bs = P.basis + (size_t)cw.ci * CCD_BASIS_STRIDE;
-        double *r = LDS().row[l];
+        double *r = L->row[l];
+        r[0] = bs[0] - (double)P.acc_t0;
 #pragma unroll
-        for (int c = 0; c < 7; ++c) r[c] = bs[c];  // bs[0] = t
+        for (int c = 1; c < 7; ++c) r[c] = bs[c];
+        r[7] = 1.0;
 #pragma unroll
-        for (int b = 0; b < NB; ++b) r[8 + b] = (double)cw.v[b];
+        for (int b = 0; b < NB; ++b) r[8 + b] = (double)((int)cw.v[b] - L->y0[b]);
+        r[15] = 0.0;
+    }
+    wsync();
+}
+
+// Raw-sum entry e of the accumulated Gram: products of staged columns (ca, cb).  0..27 design
+// x design (upper triangle), 28..76 design x band, 77..83 band x band, 84..90 design sums,
+// 91..97 band sums; e >= 98 maps to the zero column.
+__device__ __forceinline__ void gram_entry(int e, int &ca, int &cb) {
+    if (e < 28) {
+        int j = 0;
+        while (e >= 7 - j) { e -= 7 - j; ++j; }
+        ca = j;
+        cb = j + e;
+    } else if (e < 77) {
+        e -= 28;
+        ca = e / 7;
+        cb = 8 + e % 7;
+    } else if (e < 84) {
+        ca = cb = 8 + (e - 77);
+    } else if (e < 91) {
+        ca = e - 84;
+        cb = 7;
+    } else if (e < 98) {
+        ca = 8 + (e - 91);
+        cb = 7;
+    } else {
+        ca = cb = 15;
+    }
+}
+
+// Make L->S the raw sums of window [a, b): extend the accumulated window when it is a prefix of
+// [a, b) (the lookforward case: the window only grows at its end), otherwise start over with
+// the date / value shifts of observation a.  Lane = entry (two per lane), sequential over rows.
+__device__ __forceinline__ void gram_accumulate(Px &P, int a, int b) {
+    Lds *L = &LDS();
+    const int l = lane();
+    int from = P.acc_b;
+    if (!(P.acc_a == a && P.acc_b <= b)) {
+        P.acc_a = a;
+        P.acc_t0 = CDR(P, a);
+        if (l < NB) L->y0[l] = (int)CVR(P, l, a);
+        L->S[l] = 0.0;
+        if (l + W < 98) L->S[l + W] = 0.0;
+        wsync();
+        from = a;
+    }
+    P.acc_b = b;
+    if (from >= b) return;
+    int ca0, cb0, ca1, cb1;
+    gram_entry(l, ca0, cb0);
+    gram_entry(l + W, ca1, cb1);
+    double s0 = L->S[l], s1 = l + W < 98 ? L->S[l + W] : 0.0;
+    for (int t0 = from; t0 < b; t0 += TR) {
+        const int cnt = b - t0 < TR ? b - t0 : TR;
+        stage_rows(P, t0, cnt);
+        for (int r = 0; r < cnt; ++r) {
+            s0 += L->row[r][ca0] * L->row[r][cb0];
+            s1 += L->row[r][ca1] * L->row[r][cb1];
+        }
+        wsync();
+    }
+    L->S[l] = s0;
+    if (l + W < 98) L->S[l + W] = s1;
+    wsync();
+}
+
+// Centred Gram (sklearn's centred design / targets) and the means of the raw columns from the
+// raw sums of [acc_a, acc_b): entry = S_ab - S_a S_b / n; means = (shifted sum + n shift) / n
+// (exact integer shifts, so the means equal the plain column means).
+__device__ __forceinline__ void gram_finalize(const Px &P, int nw) {
+    Lds *L = &LDS();
+    const int l = lane();
+    const double n = (double)nw;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int e = l + h * W;
+        int ca, cb;
+        gram_entry(e, ca, cb);
+        if (e < 98) {
+            const double se = L->S[e];
+            if (e < 28) {
+                const double v = se - L->S[84 + ca] * (L->S[84 + cb] / n);
+                L->G[ca][cb] = v;
+                L->G[cb][ca] = v;
+            } else if (e < 77) {
+                L->Q[ca][cb - 8] = se - L->S[84 + ca] * (L->S[91 + cb - 8] / n);
+            } else if (e < 84) {
+                L->YY[ca - 8] = se - L->S[91 + ca - 8] * (L->S[91 + ca - 8] / n);
+            } else if (e < 91) {
+                L->xm[ca] = (se + (ca == 0 ? n * (double)P.acc_t0 : 0.0)) / n;
+            } else {
+                L->ym[ca - 8] = (se + n * (double)L->y0[ca - 8]) / n;
+            }
+        }
     }
     wsync();
 }
@@ -509,81 +620,19 @@ __device__ __forceinline__ double resid_at(const Px &P, int band, int j) {
 }
 
 // lasso.fitted_model for the 7 bands over compacted window [a, b) with k coefficients.
-__device__ __forceinline__ void fit_models(Px &P, int a, int b, int k) {
+// with_rmse = false leaves L->rmse to the caller (build_closest computes it from the same
+// residuals).  A window and k equal to the last fit's keep the models as they are.
+__device__ __forceinline__ void fit_models(Px &P, int a, int b, int k, bool with_rmse = true) {
     const ccdgpu_params &p = c_args.p;
     Lds *L = &LDS();
     const int l = lane();
     const int nw = b - a;
     const int pc = k - 1;  // active design columns (t + harmonics)
+    if (P.acc_a == a && P.acc_b == b && P.fit_k == k) return;  // same rows, same model
     PH_BEGIN(gram)
-    // pass 1: column means (x columns 0..6, y bands) -- sequential per column, lane = column
-    double acc = 0.0;
-    for (int t0 = 0; t0 < nw; t0 += TR) {
-        const int cnt = nw - t0 < TR ? nw - t0 : TR;
-        stage_rows(P, a + t0, cnt);
-        if (l < 14) {
-            const int col = l < 7 ? l : l + 1;
-            for (int r = 0; r < cnt; ++r) acc += L->row[r][col];
-        }
-        wsync();
-    }
-    if (l < 7) L->xm[l] = acc / nw;
-    else if (l < 14) L->ym[l - 7] = acc / nw;
-    wsync();
-    // pass 2: centred Gram entries; lane handles entries e = l and l + 64
-    const int nG = pc * (pc + 1) / 2;
-    const int nE = nG + 7 * pc + 7;
-    int ca[2], cb[2];
-    double ma[2], mb[2], s[2] = {0.0, 0.0};
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        int e = l + h * W;
-        ca[h] = cb[h] = -1;
-        ma[h] = mb[h] = 0.0;
-        if (e < nG) {
-            int j = 0;
-            while (e >= pc - j) { e -= pc - j; ++j; }
-            ca[h] = j;
-            cb[h] = j + e;
-        } else if (e < nG + 7 * pc) {
-            e -= nG;
-            ca[h] = e / 7;        // design column
-            cb[h] = 8 + e % 7;    // y band
-        } else if (e < nE) {
-            e -= nG + 7 * pc;
-            ca[h] = cb[h] = 8 + e;
-        }
-        if (ca[h] >= 0) {
-            ma[h] = ca[h] < 8 ? L->xm[ca[h]] : L->ym[ca[h] - 8];
-            mb[h] = cb[h] < 8 ? L->xm[cb[h]] : L->ym[cb[h] - 8];
-        }
-    }
-    for (int t0 = 0; t0 < nw; t0 += TR) {
-        const int cnt = nw - t0 < TR ? nw - t0 : TR;
-        if (nw > TR) stage_rows(P, a + t0, cnt);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (ca[h] >= 0) {
-                for (int r = 0; r < cnt; ++r)
-                    s[h] += (L->row[r][ca[h]] - ma[h]) * (L->row[r][cb[h]] - mb[h]);
-            }
-        }
-        wsync();
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        if (ca[h] >= 0) {
-            if (cb[h] < 8) {
-                L->G[ca[h]][cb[h]] = s[h];
-                L->G[cb[h]][ca[h]] = s[h];
-            } else if (ca[h] < 8) {
-                L->Q[ca[h]][cb[h] - 8] = s[h];
-            } else {
-                L->YY[ca[h] - 8] = s[h];
-            }
-        }
-    }
-    wsync();
+    gram_accumulate(P, a, b);
+    gram_finalize(P, nw);
+    P.fit_k = k;
     PH_END(P, gram, 4)
     PH_BEGIN(cd)
     // coordinate descent: lane = band * 8 + coordinate
@@ -609,7 +658,7 @@ __device__ __forceinline__ void fit_models(Px &P, int a, int b, int k) {
     PH_BEGIN(rmse)
     // rmse from residuals of the raw design (predict = X @ coef + intercept);
     // lane = (observation sub-index, band), 8 observations per pass
-    {
+    if (with_rmse) {
         const int bnd = l >> 3, osub = l & 7;  // band-major: DPP reduction over the 8 partials
         double ss = 0.0;
         if (bnd < NB)
@@ -1274,7 +1323,7 @@ __device__ __forceinline__ void build_hist(const Px &P, int fa, int fb) {
 
 // Counting sort of the fit window [fa, fb) by u into P.bk and the squared residuals of the
 // current models (L->coef) in bucket order into P.fs.
-__device__ __forceinline__ void build_closest(const Px &P, int fa, int fb) {
+__device__ __forceinline__ void build_closest(const Px &P, int fa, int fb, int k) {
     Lds *L = &LDS();
     const int l = lane();
     const int nf = fb - fa;
@@ -1299,8 +1348,12 @@ __device__ __forceinline__ void build_closest(const Px &P, int fa, int fb) {
         P.bk[gidx(P, pos, P.n, __LINE__)] = (uint16_t)(i - fa);
     }
     gsync();
-    // squared residuals in bucket order: lane = bucket position, all 7 bands per lane
+    // squared residuals in bucket order: lane = bucket position, all 7 bands per lane; their
+    // sums are the models' rmse (lasso.fitted_model) over the same fit window
     const Lds *Lc = L;
+    double ssq[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) ssq[b] = 0.0;
     for (int t0 = 0; t0 < nf; t0 += W) {
         const int t = t0 + l;
         if (t < nf) {
@@ -1323,8 +1376,15 @@ __device__ __forceinline__ void build_closest(const Px &P, int fa, int fb) {
                 const double y = (double)(int16_t)(qw[b >> 1] >> ((b & 1) * 16));
                 const double r = y - pr;
                 o[b] = r * r;
+                ssq[b] += r * r;
             }
         }
+    }
+    const double den = (double)(nf - (c_args.p.rmse_dof ? k : 0));
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const double t = wsum(ssq[b]);
+        if (l == b) L->rmse[b] = sqrt(t / den);
     }
     gsync();
 }
@@ -1500,6 +1560,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
     int peek_start = b;
     int moff = 0;            // ring offset of the last evaluated peek window
     int hfa = -1, hfb = -1;  // fit window the closest-DOY buckets describe
+    int nc_fit = nc;         // coefficients of the current fit
     for (;;) {
         if (!(b + k < P.m || !have)) break;
         if (!have || b - a < 24) {
@@ -1510,6 +1571,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
             fb = b;
             fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
             fit_models(P, fa, fb, nc);
+            nc_fit = nc;
             have = true;
             if (l < NB) L->comp[l] = L->rmse[l];
             wsync();
@@ -1534,7 +1596,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
         const int nf = fb - fa;
         if (nf > 24 && (hfa != fa || hfb != fb)) {
             PH_BEGIN(hb)
-            build_closest(P, fa, fb);
+            build_closest(P, fa, fb, nc_fit);
             PH_END(P, hb, 12)
             hfa = fa;
             hfb = fb;
@@ -1628,7 +1690,8 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
             fa = a;
             fb = b;
             fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
-            fit_models(P, fa, fb, nc);
+            fit_models(P, fa, fb, nc, fb - fa <= 24);  // rmse: from build_closest when it runs
+            nc_fit = nc;
         }
     }
     PH_BEGIN(md)
@@ -1801,6 +1864,9 @@ __device__ __forceinline__ void detect_body() {
         const int pix = (int)(job % (unsigned long long)A.n_pix);
         P.gpix = (int64_t)job;
         P.nseg = 0;
+        P.acc_a = -1;
+        P.acc_b = 0;
+        P.fit_k = 0;
         P.basis = as_global(A.basis + (size_t)chip * A.n_obs * CCD_BASIS_STRIDE);
         P.sd = A.sdates + (size_t)chip * A.n_obs;
         PH_BEGIN(tot)
