@@ -495,13 +495,11 @@ __device__ __forceinline__ double gsum8(double v) {
     v += dpp<0x4E>(v);
     return v + dpp<0x141>(v);
 }
+// (fmax: one v_max_f64 per level; every operand here is a non-NaN magnitude)
 __device__ __forceinline__ double gmax8(double v) {
-    double t = dpp<0xB1>(v);
-    v = t > v ? t : v;
-    t = dpp<0x4E>(v);
-    v = t > v ? t : v;
-    t = dpp<0x141>(v);
-    return t > v ? t : v;
+    v = fmax(v, dpp<0xB1>(v));
+    v = fmax(v, dpp<0x4E>(v));
+    return fmax(v, dpp<0x141>(v));
 }
 
 // Lane (group base + J) of every 8-lane group, broadcast to the whole group: quad_perm broadcast
@@ -527,8 +525,8 @@ template <int J>
 __device__ __forceinline__ void cd_coord(int k, bool live, double alpha, double gkk, double rgkk,
                                          double gcolJ, double &g, double &w) {
     const double tmp = g + gkk * w;
-    const double aa = fabs(tmp) - alpha;
-    const double wn = aa > 0.0 ? (tmp > 0.0 ? aa : -aa) * rgkk : 0.0;
+    // sklearn: fsign(tmp) * fmax(|tmp| - alpha, 0) / norm (a signed zero below alpha, as there)
+    const double wn = copysign(fmax(fabs(tmp) - alpha, 0.0), tmp) * rgkk;
     const bool upd = live && k == J;
     const double wnew = upd ? wn : w;
     const double d = wnew - w;  // 0 outside the updated lane
@@ -726,6 +724,7 @@ __device__ __forceinline__ int select_u16(F gen, int N, int k) {
     for (int pass = 0; pass < 2; ++pass) {
         for (int i = l; i < 256; i += W) L->hist2[i] = 0u;
         wsync();
+#pragma unroll 4
         for (int base = 0; base < N; base += W) {
             const int i = base + l;
             int v = 0;
@@ -783,21 +782,42 @@ __device__ __forceinline__ void variogram(Px &P) {
     }
     const int kk = lag ? lag : 1;
     const bool all = lag == 0;
+    // the qualifying absolute differences of all 7 bands, compacted once into the slot's scratch
+    // (band-major u16 [7][n]); the 7 medians then read them coalesced
+    GLOBAL_AS uint16_t *dv = reinterpret_cast<GLOBAL_AS uint16_t *>(P.fs);
+    const int stride = P.n;
     int cnt = 0;
     for (int base = 0; base < m - kk; base += W) {
         const int i = base + l;
-        cnt += popc(bal(i < m - kk && (all || (CDR(P, i + kk) - CDR(P, i)) > 30)));
+        bool ok = false;
+        uint4 r0 = {0u, 0u, 0u, 0u}, r1 = {0u, 0u, 0u, 0u};
+        if (i < m - kk) {
+            ok = all || (CDR(P, i + kk) - CDR(P, i)) > 30;
+            r0 = reinterpret_cast<const uint4 *>(PCR(P))[i];
+            r1 = reinterpret_cast<const uint4 *>(PCR(P))[i + kk];
+        }
+        const unsigned long long km = bal(ok);
+        if (ok) {
+            const int pos = cnt + below(km);
+            const unsigned a0[4] = {r0.x, r0.y, r0.z, r0.w}, a1[4] = {r1.x, r1.y, r1.z, r1.w};
+#pragma unroll
+            for (int band = 0; band < NB; ++band) {
+                const int v0 = (int)(int16_t)(a0[band >> 1] >> ((band & 1) * 16));
+                const int v1 = (int)(int16_t)(a1[band >> 1] >> ((band & 1) * 16));
+                const int d = v1 - v0;
+                dv[band * stride + pos] = (uint16_t)(d < 0 ? -d : d);
+            }
+        }
+        cnt += popc(km);
     }
+    gsync();
     for (int band = 0; band < NB; ++band) {
-        const CRow *v = PCR(P);
+        const GLOBAL_AS uint16_t *col = dv + band * stride;
         auto gen = [&](int i, int &val) -> bool {
-            if (i >= m - kk) return false;
-            if (!all && (CDR(P, i + kk) - CDR(P, i)) <= 30) return false;
-            int d = (int)v[i + kk].v[band] - (int)v[i].v[band];
-            val = d < 0 ? -d : d;
+            val = (int)col[i];
             return true;
         };
-        const double med = median_u16(gen, m - kk, cnt);
+        const double med = median_u16(gen, cnt, cnt);
         if (l == 0) L->vario[band] = med;
         P.fl += 2ull * (unsigned long long)(m - kk);  // 2 per difference per band
     }
@@ -1477,11 +1497,15 @@ __device__ __forceinline__ void ring_rows(const Px &P, int x0) {
 // Entries of the fit window whose closest-DOY bin lies within circular distance d of bin u
 // (L->hist2 = bin end positions after build_closest).
 __device__ __forceinline__ int cnt_within(const Lds *L, int nf, int u, int d) {
-    if (d >= 730) return nf;
-    const int lo = u - d, hi = u + d;
-    if (lo >= 0 && hi <= 1460) return bend(L, hi) - (lo > 0 ? bend(L, lo - 1) : 0);
-    if (lo < 0) return bend(L, hi) + nf - bend(L, lo + 1460);
-    return nf - (lo > 0 ? bend(L, lo - 1) : 0) + bend(L, hi - 1461);
+    // bins [u - d, u + d] (circular; 2 d + 1 < 1461 so at most one end wraps)
+    int lo = u - d;
+    lo += lo < 0 ? 1461 : 0;
+    int hi = u + d;
+    hi -= hi > 1460 ? 1461 : 0;
+    const int eh = bend(L, hi);
+    const int el = bend(L, lo > 0 ? lo - 1 : 0);
+    const int c = eh - (lo > 0 ? el : 0) + (lo > hi ? nf : 0);
+    return d >= 730 ? nf : c;
 }
 
 // Per-lane find_closest_doy(period, ref, fit_window, 24) comparison rmse (change.lookforward):
@@ -1627,11 +1651,14 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
             PH_END(P, cmp, 14)
             PH_BEGIN(mg)
             const double *R = PRES(L) + l;
-            double rmv[NB];
+            // change_magnitude: (r / max(vario, comp))^2 summed over the detection bands, with the
+            // division as a multiply by the band's reciprocal (one division per band and step)
+            double irm[NB];
 #pragma unroll
             for (int bd = 0; bd < NB; ++bd) {
                 const double vr = L->vario[bd], cr = cs[bd];
-                rmv[bd] = (vr != vr || cr != cr) ? __builtin_nan("") : (vr > cr ? vr : cr);
+                const double rm = (vr != vr || cr != cr) ? __builtin_nan("") : (vr > cr ? vr : cr);
+                irm[bd] = ((p.detection_bands >> bd) & 1u) ? 1.0 / rm : 0.0;
             }
             allc = true;
             for (int jj = 0; jj < k; ++jj) {
@@ -1639,7 +1666,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
 #pragma unroll
                 for (int bd = 0; bd < NB; ++bd) {
                     if ((p.detection_bands >> bd) & 1u) {
-                        const double v = R[bd * W + jj] / rmv[bd];
+                        const double v = R[bd * W + jj] * irm[bd];
                         mg += v * v;
                     }
                 }
@@ -1923,10 +1950,13 @@ __device__ __forceinline__ void detect_body() {
     }
 }
 
-// Two register budgets of the same body: occupancy-1 (no spills) and 4 waves/SIMD (128 VGPRs,
-// the compiler spills the rest).  The host picks one (CCDGPU_KERNEL=w1|w4; default w4).
+// Three register budgets of the same body: 1 wave/SIMD (no spills), 2 and 3 waves/SIMD (256 and
+// 168 VGPRs, some spills).  The host picks one (CCDGPU_KERNEL=w1|w2|w3; default w3, the fastest).
+// A 4-waves/SIMD build (128 VGPRs) was dropped: its code generation broke golden parity
+// (deterministically, on every golden case), while w1..w3 of the same source match.
 __global__ __launch_bounds__(64) __attribute__((flatten)) void ccd_detect() { detect_body(); }
-__global__ __launch_bounds__(64, 4) __attribute__((flatten)) void ccd_detect_w4() { detect_body(); }
+__global__ __launch_bounds__(64, 2) __attribute__((flatten)) void ccd_detect_w2() { detect_body(); }
+__global__ __launch_bounds__(64, 3) __attribute__((flatten)) void ccd_detect_w3() { detect_body(); }
 
 // ------------------------------------------------------------------ per-chip preparation
 // One 256-thread block per chip: stable rank of each date (ties by input position), sorted
@@ -2015,7 +2045,11 @@ extern "C" size_t ccdk_lds_bytes(int32_t n_obs) {
 }
 
 static const void *detect_fn(int variant) {
-    return variant == 1 ? reinterpret_cast<const void *>(&ccd_detect) : reinterpret_cast<const void *>(&ccd_detect_w4);
+    switch (variant) {
+    case 1: return reinterpret_cast<const void *>(&ccd_detect);
+    case 2: return reinterpret_cast<const void *>(&ccd_detect_w2);
+    default: return reinterpret_cast<const void *>(&ccd_detect_w3);
+    }
 }
 
 // resident waves per CU for this variant and period length (0 on error)
@@ -2030,10 +2064,11 @@ extern "C" int ccdk_occupancy(int variant, int32_t n_obs) {
 
 extern "C" int ccdk_detect(int32_t grid, int variant, int32_t n_obs, void *stream) {
     const size_t lds = ccdk_lds_bytes(n_obs);
-    if (variant == 1)
-        hipLaunchKernelGGL(ccd_detect, dim3(grid), dim3(64), lds, (hipStream_t)stream);
-    else
-        hipLaunchKernelGGL(ccd_detect_w4, dim3(grid), dim3(64), lds, (hipStream_t)stream);
+    switch (variant) {
+    case 1: hipLaunchKernelGGL(ccd_detect, dim3(grid), dim3(64), lds, (hipStream_t)stream); break;
+    case 2: hipLaunchKernelGGL(ccd_detect_w2, dim3(grid), dim3(64), lds, (hipStream_t)stream); break;
+    default: hipLaunchKernelGGL(ccd_detect_w3, dim3(grid), dim3(64), lds, (hipStream_t)stream); break;
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

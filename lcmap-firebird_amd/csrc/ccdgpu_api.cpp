@@ -81,7 +81,7 @@ struct ccdgpu_ctx {
     int device = 0;
     int n_cu = 0;
     int slots_per_cu = 0;
-    int variant = 4;  // detection kernel register budget: 1 or 4 waves/SIMD (CCDGPU_KERNEL)
+    int variant = 3;  // detection kernel register budget: 1..3 waves/SIMD (CCDGPU_KERNEL=w1..w3)
     hipStream_t stream = nullptr;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // staged batch
@@ -214,8 +214,10 @@ int ccdgpu_init(int device, ccdgpu_ctx **out) {
     }
     for (auto &e : c->ev) (void)hipEventCreate(&e);
     c->slots_per_cu = 16;
-    c->variant = ccdk_period_in_lds() ? 1 : 4;
-    if (const char *v = std::getenv("CCDGPU_KERNEL")) c->variant = (std::strcmp(v, "w1") == 0) ? 1 : 4;
+    c->variant = ccdk_period_in_lds() ? 1 : 3;
+    if (const char *v = std::getenv("CCDGPU_KERNEL")) {
+        if (v[0] == 'w' && v[1] >= '1' && v[1] <= '3' && v[2] == 0) c->variant = v[1] - '0';
+    }
     if (const char *v = std::getenv("CCDGPU_SLOTS_PER_CU")) c->slots_per_cu = std::max(1, std::atoi(v));
     *out = c;
     return 0;
