@@ -77,6 +77,15 @@ struct __attribute__((aligned(16))) Lds {
 // Launch arguments live in constant memory (uniform scalar loads from every device function);
 // the per-wave LDS block is the dynamic shared segment (so every access is a ds_* instruction).
 __constant__ CcdDetectArgs c_args;
+// Every device function reads the launch arguments through ARGS(): the opaque zero index keeps
+// the compiler from hoisting the (invariant) constant loads to the top of the persistent kernel,
+// where they would stay live in SGPRs for its whole length and be spilled; re-reading them at
+// the use is a scalar-cache hit.
+__device__ __forceinline__ const CcdDetectArgs &ARGS() {
+    int z = 0;
+    asm volatile("" : "+s"(z));
+    return (&c_args)[z];
+}
 extern __shared__ __attribute__((aligned(16))) char ccd_smem[];
 __device__ __forceinline__ Lds &LDS() { return *reinterpret_cast<Lds *>(ccd_smem); }
 // Peek-residual ring, band-major [band][64 observations], in the row staging tile (the Gram
@@ -190,7 +199,13 @@ __device__ __forceinline__ CRow crow(const Px &P, int j, int line) {
 #define CVR(P, b, j) cvr(P, (b), (j), __LINE__)
 
 // ------------------------------------------------------------------ wave primitives
-__device__ __forceinline__ int lane() { return (int)__lane_id(); }
+// Opaque like ARGS(): lane-derived masks and index maps are recomputed where they are used
+// instead of being hoisted to the kernel entry and kept live (spilled) for the whole kernel.
+__device__ __forceinline__ int lane() {
+    int l = (int)__lane_id();
+    asm volatile("" : "+v"(l));
+    return l;
+}
 __device__ __forceinline__ unsigned long long bal(bool p) { return __ballot(p); }
 __device__ __forceinline__ int popc(unsigned long long x) { return __popcll(x); }
 __device__ __forceinline__ int below(unsigned long long m) {
@@ -621,7 +636,7 @@ __device__ __forceinline__ double resid_at(const Px &P, int band, int j) {
 // with_rmse = false leaves L->rmse to the caller (build_closest computes it from the same
 // residuals).  A window and k equal to the last fit's keep the models as they are.
 __device__ __forceinline__ void fit_models(Px &P, int a, int b, int k, bool with_rmse = true) {
-    const ccdgpu_params &p = c_args.p;
+    const ccdgpu_params &p = ARGS().p;
     Lds *L = &LDS();
     const int l = lane();
     const int nw = b - a;
@@ -676,7 +691,7 @@ __device__ __forceinline__ void fit_models(Px &P, int a, int b, int k, bool with
 // ------------------------------------------------------------------ segment output
 __device__ __forceinline__ void emit(Px &P, int sday, int eday, int bday, int count, double chprob, int cqa,
                      double mag_lane /* lane b: magnitude of band b */) {
-    const CcdDetectArgs &A = c_args;
+    const CcdDetectArgs &A = ARGS();
     const int l = lane();
     unsigned long long slot = 0;
     if (l == 0) slot = atomicAdd(&A.counters[1], 1ull);
@@ -708,7 +723,7 @@ __device__ __forceinline__ void emit(Px &P, int sday, int eday, int bday, int co
 }
 
 __device__ __forceinline__ void catch_(Px &P, int a, int b, int cqa) {
-    fit_models(P, a, b, c_args.p.coef_min);
+    fit_models(P, a, b, ARGS().p.coef_min);
     const int bday = b < P.m ? CDR(P, b) : CDR(P, P.m - 1);
     emit(P, CDR(P, a), CDR(P, b - 1), bday, b - a, 0.0, cqa, 0.0);
 }
@@ -825,7 +840,7 @@ __device__ __forceinline__ void variogram(Px &P) {
 }
 
 __device__ __forceinline__ void adjust_peek(Px &P) {
-    const ccdgpu_params &p = c_args.p;
+    const ccdgpu_params &p = ARGS().p;
     P.peek = p.peek_size;
     P.chg = p.change_threshold;
     if (!p.adaptive_peek || P.m < 2) return;
@@ -838,7 +853,7 @@ __device__ __forceinline__ void adjust_peek(Px &P) {
     const double adj = rint((double)(p.peek_size * 16) / delta);
     if (adj > (double)p.peek_size) {
         P.peek = adj > (double)CCDGPU_MAX_PEEK ? CCDGPU_MAX_PEEK : (int)adj;
-        P.chg = c_args.thr_table[P.peek];
+        P.chg = ARGS().thr_table[P.peek];
     }
 }
 
@@ -990,7 +1005,7 @@ __device__ __forceinline__ void tm_trig(const Px &P, int a, int nw, double oc, G
 
 // Returns the outlier count; outlier flags in L->tflag (bit i = window observation i).
 __device__ __forceinline__ int tmask(Px &P, int a, int b) {
-    const ccdgpu_params &p = c_args.p;
+    const ccdgpu_params &p = ARGS().p;
     Lds *L = &LDS();
     const int l = lane();
     const int nw = b - a;
@@ -1142,7 +1157,7 @@ __device__ __forceinline__ int num_coefs(const ccdgpu_params &p, int n) {
 }
 
 __device__ __forceinline__ bool stable(const Px &P, int a, int b) {
-    const ccdgpu_params &p = c_args.p;
+    const ccdgpu_params &p = ARGS().p;
     const Lds *L = &LDS();
     const int l = lane();
     double v2 = 0.0;
@@ -1159,7 +1174,7 @@ __device__ __forceinline__ bool stable(const Px &P, int a, int b) {
 __device__ __forceinline__ void count_stable(Px &P) {}
 
 __device__ __forceinline__ bool initialize(Px &P, int &wa, int &wb) {
-    const ccdgpu_params &p = c_args.p;
+    const ccdgpu_params &p = ARGS().p;
     const Lds *L = &LDS();
     const int l = lane();
     int a = wa, b = wb;
@@ -1211,7 +1226,7 @@ __device__ __forceinline__ bool initialize(Px &P, int &wa, int &wb) {
 // for the segment's magnitude medians.  Returns true iff every peek observation exceeds the
 // change threshold (change.detect_change); mag0 = magnitude of observation 0 (detect_outlier).
 __device__ __forceinline__ bool eval_peek(Px &P, int k, int start, int dir, double &mag0) {
-    const ccdgpu_params &p = c_args.p;
+    const ccdgpu_params &p = ARGS().p;
     Lds *L = &LDS();
     const int l = lane();
     const int bnd = l & 7, osub = l >> 3;
@@ -1278,7 +1293,7 @@ __device__ __forceinline__ double peek_medians(Px &P, int k, int off) {
 }
 
 __device__ __forceinline__ void lookback(Px &P, int &wa, int &wb, int prev) {
-    const ccdgpu_params &p = c_args.p;
+    const ccdgpu_params &p = ARGS().p;
     const int l = lane();
     int a = wa, b = wb;
     if (l < NB) LDS().comp[l] = LDS().rmse[l];  // change.lookback: comparison rmse = model rmse
@@ -1400,7 +1415,7 @@ __device__ __forceinline__ void build_closest(const Px &P, int fa, int fb, int k
             }
         }
     }
-    const double den = (double)(nf - (c_args.p.rmse_dof ? k : 0));
+    const double den = (double)(nf - (ARGS().p.rmse_dof ? k : 0));
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
         const double t = wsum(ssq[b]);
@@ -1570,7 +1585,7 @@ __device__ __forceinline__ void comp_lane(const Px &P, int nf, int dref, double 
 // needs a refit (span test on the last kept observation before it) or detects a change.
 // Removals are applied in one compaction pass per batch.
 __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
-    const ccdgpu_params &p = c_args.p;
+    const ccdgpu_params &p = ARGS().p;
     Lds *L = &LDS();
     const int l = lane();
     const int k = P.peek;
@@ -1730,7 +1745,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
 }
 
 __device__ __forceinline__ void standard_procedure(Px &P) {
-    const ccdgpu_params &p = c_args.p;
+    const ccdgpu_params &p = ARGS().p;
     const int meow = p.meow_size;
     PH_BEGIN(vg)
     variogram(P);
@@ -1760,7 +1775,7 @@ __device__ __forceinline__ void standard_procedure(Px &P) {
 // ------------------------------------------------------------------ qa.py filters + compaction
 // Returns the procedure, or -1 for an unsupported QA value.
 __device__ __forceinline__ int px_setup(Px &P, int chip, int pix) {
-    const CcdDetectArgs &A = c_args;
+    const CcdDetectArgs &A = ARGS();
     const ccdgpu_params &p = A.p;
     Lds *L = &LDS();
     const int l = lane();
@@ -1862,7 +1877,7 @@ __device__ __forceinline__ int px_setup(Px &P, int chip, int pix) {
 }
 
 __device__ __forceinline__ void detect_body() {
-    const CcdDetectArgs &A = c_args;
+    const CcdDetectArgs &A = ARGS();
     Lds &lds = LDS();
     const int l = lane();
     const int slot = blockIdx.x;

@@ -4,8 +4,8 @@ MI355X guide's gfx950 correction + WRITE_SIZE), derived rates.  Developer tool (
 import csv, glob, json, os, sys
 from collections import defaultdict
 
-tag = sys.argv[1] if len(sys.argv) > 1 else 'pmc'
-root = sys.argv[2] if len(sys.argv) > 2 else 'gpurun_out'
+tag = sys.argv[1] if len(sys.argv) > 1 else "pmc"
+root = "gpurun_out"
 kern = 'ccd_detect'
 vals = defaultdict(list)
 dur = []
@@ -35,3 +35,16 @@ for a, b in (('SQ_WAIT_ANY', 'SQ_WAVE_CYCLES'), ('SQ_ACTIVE_INST_ANY', 'SQ_WAVE_
     if a in out and b in out and out[b]:
         out[a + '/' + b] = out[a] / out[b]
 print(json.dumps(out, indent=1))
+
+# --write <workload>: record the per-launch HBM traffic for bench.py's roofline.traffic field
+if '--write' in sys.argv:
+    wl = sys.argv[sys.argv.index('--write') + 1]
+    rec = {'workload': wl, 'kernel': kern, 'source': 'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, tag %s' % tag,
+           'hbm_bytes_per_launch': out.get('hbm_bytes_per_launch'),
+           'hbm_read_bytes': out.get('hbm_read_bytes'), 'hbm_write_bytes': out.get('hbm_write_bytes'),
+           'correction': 'FETCH_SIZE x 2 (gfx950 reports half the bytes of wide reads, MI355X_MICROARCH.md HBM section); WRITE_SIZE as read',
+           'counters': {k: v for k, v in out.items() if k.isupper() or k.startswith('SQ_') or k.startswith('TC')}}
+    os.makedirs(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'profiles'), exist_ok=True)
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'profiles', 'pmc_detect.json')
+    json.dump(rec, open(path, 'w'), indent=1)
+    print('wrote', path)
