@@ -63,6 +63,9 @@ struct __attribute__((aligned(16))) Lds {
     double med1[8], med2[8];
     uint32_t mask[MAXW];   // processing mask, sorted order
     int sel[32];           // compacted indices of the 24 closest-DOY observations
+#ifdef CCD_PHASE_TIMERS
+    unsigned long long tph[CCD_NPHASE];  // diagnostic build: per-phase cycle totals of this wave
+#endif
     double S[98];          // raw Gram sums of the accumulated window (entry map: gram_entry)
     int y0[8];             // per-band value shift of the accumulated window
     union {                // Tmask (initialize) and the closest-DOY buckets (lookforward) never overlap
@@ -124,9 +127,6 @@ struct Px {
     unsigned long long fl;       // counted FP64 flops, wave-uniform part
     unsigned long long fl_lane;  // counted FP64 flops, per-lane part (coordinate descent)
     mutable int bad;             // source line of a tripped index guard (0 = none), per lane
-#ifdef CCD_PHASE_TIMERS
-    unsigned long long tph[CCD_NPHASE];
-#endif
 };
 
 // Where the compacted period lives.  CCD_PERIOD_IN_LDS: in the wave's LDS block right after the
@@ -162,8 +162,10 @@ __device__ __forceinline__ unsigned long long ph_stamp() {
     return t;
 }
 #define PH_BEGIN(id) const unsigned long long _ph_##id = ph_stamp();
-#define PH_END(P, id, slot) (P).tph[slot] += ph_stamp() - _ph_##id;
-#define PH_COUNT(P, slot, v) (P).tph[slot] += (unsigned long long)(v);
+// (totals live in LDS, not in the pixel state, so the diagnostic build keeps the product's
+// register allocation as far as possible; lane 0 accumulates)
+#define PH_END(P, id, slot) { const unsigned long long _d = ph_stamp() - _ph_##id; if (lane() == 0) LDS().tph[slot] += _d; }
+#define PH_COUNT(P, slot, v) { if (lane() == 0) LDS().tph[slot] += (unsigned long long)(v); }
 #else
 #define PH_COUNT(P, slot, v)
 #define PH_BEGIN(id)
@@ -1895,7 +1897,7 @@ __device__ __forceinline__ void detect_body() {
     P.fl = 0;
     P.fl_lane = 0;
 #ifdef CCD_PHASE_TIMERS
-    for (int i = 0; i < CCD_NPHASE; ++i) P.tph[i] = 0;
+    if (l < CCD_NPHASE) lds.tph[l] = 0;
 #endif
     for (;;) {
         unsigned long long job = 0;
@@ -1960,7 +1962,7 @@ __device__ __forceinline__ void detect_body() {
         atomicAdd(&A.stats[1], sw);
         atomicAdd(&A.stats[2], P.fl + fll);
 #ifdef CCD_PHASE_TIMERS
-        for (int i = 0; i < CCD_NPHASE; ++i) atomicAdd(&A.stats[8 + i], P.tph[i]);
+        for (int i = 0; i < CCD_NPHASE; ++i) atomicAdd(&A.stats[8 + i], lds.tph[i]);
 #endif
     }
 }
