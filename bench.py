@@ -164,7 +164,8 @@ def main():
             'unit': 'TFLOP/s',
             'frac': achieved_tf / FP64_PEAK_TFLOPS,
             'traffic': traffic,
-            'kernel': 'ccd_detect',
+            'kernel': {'w1': 'ccd_detect', 'w2': 'ccd_detect_w2'}.get(os.environ.get('CCDGPU_KERNEL', 'w3'), 'ccd_detect_w3'),
+            'traffic_note': 'traffic = HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE (profiles/pmc_detect.json); mostly per-wave scratch (compacted period, closest-DOY buckets) re-read from HBM',
             'kernel_ms_per_launch': det_avg,
             'flops_per_launch': flops,
             'algorithmic_bytes_per_launch': alg_bytes,
