@@ -124,6 +124,24 @@ void ccdgpu_result_free(ccdgpu_result *out);
 int ccdgpu_stage(ccdgpu_ctx *ctx, const ccdgpu_params *params, int32_t n_chips, int32_t n_pix,
                  int32_t n_obs, const int64_t *dates, const int16_t *spectra, const uint16_t *qa);
 int ccdgpu_run_staged(ccdgpu_ctx *ctx, double *kernel_seconds);
+
+/* Chip packer: stage a batch straight from the chipmunk wire format (replaces merlin.create's
+ * per-pixel pivot and the repartition shuffle of ccdc/timeseries.py:120-125; payloads as in the
+ * reference fixture test/data/chip_response.json).  Layer l (0..6 = blues, greens, reds, nirs,
+ * swir1s, swir2s, thermals; 7 = pixel QA) of observation o of chip c is the base64 text (standard
+ * alphabet, '=' padded) starting at byte text_offsets[(c * n_obs + o) * 8 + l] of `text`; it
+ * decodes to n_pix little-endian int16 (uint16 for QA) values in row-major pixel order.  A
+ * negative offset is a missing layer: its pixels become fill (-9999, QA 1).  dates as in
+ * ccdgpu_stage.  The text is copied to the device, decoded and pivoted there to the
+ * [7][n_pix][n_obs] / [n_pix][n_obs] layout; *unpack_seconds (may be NULL) gets the kernel time.
+ * CCDGPU_EINVAL for a payload that runs past text_bytes or is not base64. */
+int ccdgpu_stage_chipmunk(ccdgpu_ctx *ctx, const ccdgpu_params *params, int32_t n_chips, int32_t n_pix,
+                          int32_t n_obs, const int64_t *dates, const char *text, int64_t text_bytes,
+                          const int64_t *text_offsets, double *unpack_seconds);
+
+/* Copy the staged pixel inputs back to the host in the ccdgpu_stage layout (spectra
+ * [n_chips][7][n_pix][n_obs], qa [n_chips][n_pix][n_obs]); either pointer may be NULL. */
+int ccdgpu_staged_inputs(ccdgpu_ctx *ctx, int16_t *spectra, uint16_t *qa);
 int ccdgpu_fetch_staged(ccdgpu_ctx *ctx, int32_t chip, ccdgpu_result *out);
 
 /* Kernel statistics of the last run (per launch of the main detection kernel). */

@@ -203,6 +203,44 @@ def detect_partition(records, params=None):
     return rows
 
 
+def detect_chips(chips, params=None, context=None):
+    """Change detection straight from chipmunk chips (the wire format merlin.create consumes in
+    timeseries.rdd, timeseries.py:120): chips of any number of locations, grouped by location,
+    batched by shared date vector, decoded and pivoted on the device (ccdc.chipmunk,
+    ccdgpu.Context.stage_chipmunk) and detected there.  Returns the rows ``detect`` would give
+    for every pixel of every location (pixel keys as test/__init__.py:37: px = cx + 30 col,
+    py = cy - 30 row), locations in first-seen order.  Raises ValueError (QAValueError) on an
+    unsupported QA value, like ccd.detect."""
+    import ccdgpu
+    from ccdgpu import abi
+    from ccdc import chipmunk, timeseries
+    groups = chipmunk.group(chips)
+    ctx = context or ccdgpu.default_context()
+    batches = {}
+    for key, layers in groups.items():
+        d = chipmunk.dates_of(layers)
+        batches.setdefault(d.tobytes(), []).append((key, layers))
+    rows = {}
+    for members in batches.values():
+        dates, text, offsets = chipmunk.pack_text([layers for _, layers in members])
+        first_payload = next(v for _, layers in members for n in chipmunk.LAYERS for v in layers[n].values())
+        n_pix = chipmunk.payload_pixels(first_payload)
+        ctx.stage_chipmunk(dates, text, offsets, n_pix, params)
+        ctx.run()
+        dlist = [int(x) for x in dates[0]]
+        for c, ((cx, cy), _) in enumerate(members):
+            u = ctx.fetch(c)
+            if u.error_pixel >= 0:
+                err = ccdgpu.QAValueError('unsupported QA value at pixel %d of chip (%d, %d)' % (u.error_pixel, cx, cy))
+                raise err
+            out = []
+            for px, (_, _, ppx, ppy) in enumerate(timeseries.chip_keys(cx, cy, n_pix)):
+                out.extend(format(cx=cx, cy=cy, px=ppx, py=ppy, dates=dlist,
+                                  ccdresult=abi.pixel_result(u, px, ccd.algorithm)))
+            rows[(cx, cy)] = out
+    return [r for key in groups for r in rows[key]]
+
+
 def rdd(ctx, timeseries):
     """Run change detection against an RDD of timeseries (pyccd.py:171-183)."""
     logger(context=ctx, name=__name__).info('executing change detection...')

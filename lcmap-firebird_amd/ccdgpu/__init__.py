@@ -45,12 +45,17 @@ def _declare(L):
     L.ccdgpu_result_free.argtypes = [c.POINTER(abi.Result)]
     L.ccdgpu_stage.argtypes = [c.c_void_p, c.POINTER(abi.Params), c.c_int32, c.c_int32, c.c_int32,
                                c.c_void_p, c.c_void_p, c.c_void_p]
+    L.ccdgpu_stage_chipmunk.argtypes = [c.c_void_p, c.POINTER(abi.Params), c.c_int32, c.c_int32, c.c_int32,
+                                        c.c_void_p, c.c_char_p, c.c_int64, c.c_void_p,
+                                        c.POINTER(c.c_double)]
+    L.ccdgpu_staged_inputs.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p]
     L.ccdgpu_run_staged.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
     L.ccdgpu_fetch_staged.argtypes = [c.c_void_p, c.c_int32, c.POINTER(abi.Result)]
     L.ccdgpu_last_stats.argtypes = [c.c_void_p, c.POINTER(abi.Stats)]
     L.ccdgpu_diag_counters.argtypes = [c.c_void_p, c.POINTER(c.c_uint64), c.c_int32]
     for name in ('ccdgpu_init', 'ccdgpu_destroy', 'ccdgpu_device_count', 'ccdgpu_synchronize',
-                 'ccdgpu_detect_batch', 'ccdgpu_stage', 'ccdgpu_run_staged', 'ccdgpu_fetch_staged',
+                 'ccdgpu_detect_batch', 'ccdgpu_stage', 'ccdgpu_stage_chipmunk', 'ccdgpu_staged_inputs',
+                 'ccdgpu_run_staged', 'ccdgpu_fetch_staged',
                  'ccdgpu_last_stats', 'ccdgpu_diag_counters'):
         getattr(L, name).restype = c.c_int
     return L
@@ -58,7 +63,8 @@ def _declare(L):
 
 EXPORTS = ('ccdgpu_version', 'ccdgpu_last_error', 'ccdgpu_params_default', 'ccdgpu_init',
            'ccdgpu_destroy', 'ccdgpu_device_count', 'ccdgpu_synchronize', 'ccdgpu_detect_batch',
-           'ccdgpu_result_free', 'ccdgpu_stage', 'ccdgpu_run_staged', 'ccdgpu_fetch_staged',
+           'ccdgpu_result_free', 'ccdgpu_stage', 'ccdgpu_stage_chipmunk', 'ccdgpu_staged_inputs',
+           'ccdgpu_run_staged', 'ccdgpu_fetch_staged',
            'ccdgpu_last_stats', 'ccdgpu_diag_counters')
 
 
@@ -161,6 +167,41 @@ class Context(object):
         _check(lib().ccdgpu_stage(self._ctx, ctypes.byref(p), n_chips, n_pix, n_obs,
                                   dates.ctypes.data, spectra.ctypes.data, qa.ctypes.data))
         self._keep = (dates, spectra, qa)
+        self._n_pix = n_pix
+
+    def stage_chipmunk(self, dates, text, offsets, n_pix, params=None):
+        """Stage chips from the chipmunk wire format (see ccdc.chipmunk.pack_text):
+        dates [C][n] int64, text bytes (concatenated base64 payloads), offsets [C][n][8] int64
+        byte offsets of each layer's payload (-1 = missing layer).  Decoding and the pivot to
+        the detection layout run on the device; returns the unpack kernel time in seconds."""
+        dates = np.ascontiguousarray(dates, dtype=np.int64)
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        if dates.ndim == 1:
+            dates = dates[None]
+        if offsets.ndim == 2:
+            offsets = offsets[None]
+        n_chips, n_obs = dates.shape
+        if offsets.shape != (n_chips, n_obs, 8):
+            raise ValueError('offsets must be [n_chips][n_obs][8], got %r' % (offsets.shape,))
+        text = bytes(text)
+        p = params if isinstance(params, abi.Params) else abi.params_from_dict(params)
+        secs = ctypes.c_double(0.0)
+        _check(lib().ccdgpu_stage_chipmunk(self._ctx, ctypes.byref(p), n_chips, int(n_pix), n_obs,
+                                           dates.ctypes.data, text, len(text), offsets.ctypes.data,
+                                           ctypes.byref(secs)))
+        self._keep = (dates, text, offsets)
+        self._n_pix = int(n_pix)
+        return secs.value
+
+    def staged_inputs(self):
+        """The staged pixel inputs copied back: (spectra [C][7][n_pix][n], qa [C][n_pix][n])."""
+        d = self._keep[0]
+        n_chips, n_obs = d.shape if d.ndim == 2 else (1, d.shape[0])
+        n_pix = self._n_pix
+        spectra = np.empty((n_chips, 7, n_pix, n_obs), dtype=np.int16)
+        qa = np.empty((n_chips, n_pix, n_obs), dtype=np.uint16)
+        _check(lib().ccdgpu_staged_inputs(self._ctx, spectra.ctypes.data, qa.ctypes.data))
+        return spectra, qa
 
     def run(self):
         secs = ctypes.c_double(0.0)

@@ -69,6 +69,10 @@ int ccdk_period_in_lds(void);
 // dynamic LDS bytes per wave and resident waves per CU for a period of n_obs observations
 size_t ccdk_lds_bytes(int32_t n_obs);
 int ccdk_occupancy(int variant, int32_t n_obs);
+// chipmunk wire format -> spectra / qa (ccd_pack.hip); err: set to 1 on invalid base64
+int ccdk_unpack_b64(const unsigned char *text, int64_t text_bytes, const int64_t *offsets, int32_t n_chips,
+                    int32_t n_obs, int32_t n_pix, int16_t *spectra, uint16_t *qa, unsigned long long *err,
+                    void *stream);
 int ccdk_scatter(const ccdgpu_segment *pool, const int32_t *pool_seq, int64_t n_pool,
                  const int64_t *offsets, int32_t n_pix_per_chip, ccdgpu_segment *out, void *stream);
 #ifdef __cplusplus

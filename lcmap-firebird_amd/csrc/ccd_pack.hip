@@ -1,0 +1,114 @@
+// ccd_pack.hip -- MI355X (gfx950) chip packer: chipmunk wire format -> the detection kernel's
+// band-major, observation-contiguous input buffers, on the device.
+//
+// Reference: ccdc/timeseries.py:120-125 builds per-pixel records with merlin.create (chipmunk
+// chips per ubid and acquisition date, base64 int16/uint16 100x100 payloads; fixtures
+// test/data/chip_response.json + registry_response.json) and then re-partitions them across
+// the cluster.  Here the payloads of a chip's layers (7 spectral + pixel QA) for all of its
+// acquisition dates are copied to HBM as text and one kernel decodes and pivots them:
+//
+//   text[(chip, obs, layer) payload]  base64 of n_pix little-endian 16-bit values, pixel order
+//   -> spectra[chip][band][pix][obs] int16, qa[chip][pix][obs] uint16  (include/ccdgpu.h layout)
+//
+// One 256-thread block per (chip, layer, tile of 64 observations, tile of 96 pixels): 96 pixels
+// are 192 bytes = 64 base64 quanta, so each observation row of the tile is one wave-wide decode
+// (lane = 4-character quantum -> 3 bytes into LDS); the tile is then written pixel-major with
+// consecutive threads on consecutive observations (128-byte runs per pixel).  HBM-bound byte
+// work: no MFMA, no FP.  A missing layer (offset < 0) decodes as fill (-9999, QA bit 0 = fill).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int OBS_T = 64;   // observations per tile
+constexpr int PIX_T = 96;   // pixels per tile = 192 bytes = 64 base64 quanta
+constexpr int QUANTA = PIX_T * 2 / 3;
+constexpr int NLAYER = 8;   // blues greens reds nirs swir1s swir2s thermals qas
+
+// base64 character -> 6-bit value; 64 for '=' (padding), 255 for anything else
+__device__ __forceinline__ unsigned b64v(unsigned c) {
+    if (c >= 'A' && c <= 'Z') return c - 'A';
+    if (c >= 'a' && c <= 'z') return c - 'a' + 26;
+    if (c >= '0' && c <= '9') return c - '0' + 52;
+    if (c == '+') return 62;
+    if (c == '/') return 63;
+    if (c == '=') return 64;
+    return 255;
+}
+
+__global__ __launch_bounds__(256) void ccd_unpack_b64(const unsigned char *__restrict__ text, int64_t text_bytes,
+                                                       const int64_t *__restrict__ offsets, int n_obs, int n_pix,
+                                                       int16_t *__restrict__ spectra, uint16_t *__restrict__ qa,
+                                                       unsigned long long *__restrict__ err) {
+    __shared__ uint16_t tile[OBS_T][PIX_T + 2];  // +2: odd row pitch in 32-bit words
+    const int ptile = blockIdx.x, otile = blockIdx.y;
+    const int chip = blockIdx.z / NLAYER, layer = blockIdx.z % NLAYER;
+    const int p0 = ptile * PIX_T, o0 = otile * OBS_T;
+    const int tid = threadIdx.x;
+    const int nbytes = 2 * n_pix;                    // decoded payload bytes
+    const int64_t nchars = 4 * (int64_t)((nbytes + 2) / 3);  // encoded length incl. padding
+    const uint16_t fill = layer == NLAYER - 1 ? (uint16_t)1 : (uint16_t)(int16_t)-9999;
+    bool bad = false;
+    // decode: thread -> (observation row, quantum); 64 rows x 64 quanta per tile
+    for (int e = tid; e < OBS_T * QUANTA; e += 256) {
+        const int r = e / QUANTA, q = e % QUANTA;
+        const int o = o0 + r;
+        if (o >= n_obs) continue;
+        const int64_t off = offsets[((int64_t)chip * n_obs + o) * NLAYER + layer];
+        const int64_t qg = (int64_t)ptile * QUANTA + q;  // quantum index within the payload
+        uint16_t *row = tile[r];
+        const int pb = 3 * q;                            // first decoded byte of this quantum, tile-relative
+        unsigned char by[3] = {0, 0, 0};
+        bool have = false;
+        if (off >= 0 && 4 * qg < nchars) {
+            const int64_t at = off + 4 * qg;
+            if (at + 4 <= text_bytes) {
+                const unsigned v0 = b64v(text[at]), v1 = b64v(text[at + 1]);
+                const unsigned v2 = b64v(text[at + 2]), v3 = b64v(text[at + 3]);
+                bad |= (v0 | v1) >= 64 || v2 > 64 || v3 > 64;
+                const unsigned w = (v0 << 18) | (v1 << 12) | ((v2 & 63) << 6) | (v3 & 63);
+                by[0] = (unsigned char)(w >> 16);
+                by[1] = (unsigned char)(w >> 8);
+                by[2] = (unsigned char)w;
+                have = true;
+            } else {
+                bad = true;
+            }
+        }
+        // bytes of this quantum -> 16-bit little-endian pixel values of the tile row
+        for (int k = 0; k < 3; ++k) {
+            const int b = pb + k;
+            const int pix = b >> 1;
+            if (pix >= PIX_T) continue;
+            unsigned char *rb = reinterpret_cast<unsigned char *>(row);
+            rb[b] = have ? by[k] : (unsigned char)((b & 1) ? (fill >> 8) : (fill & 0xFF));
+        }
+    }
+    __syncthreads();
+    // write: thread -> (pixel, observation), observations fastest (contiguous per pixel)
+    const bool is_qa = layer == NLAYER - 1;
+    const int64_t pstride = n_obs;
+    for (int e = tid; e < PIX_T * OBS_T; e += 256) {
+        const int pl = e / OBS_T, r = e % OBS_T;
+        const int pix = p0 + pl, o = o0 + r;
+        if (pix >= n_pix || o >= n_obs) continue;
+        const uint16_t v = tile[r][pl];
+        if (is_qa)
+            qa[((int64_t)chip * n_pix + pix) * pstride + o] = v;
+        else
+            spectra[(((int64_t)chip * 7 + layer) * n_pix + pix) * pstride + o] = (int16_t)v;
+    }
+    if (bad) atomicOr(err, 1ull);
+}
+
+}  // namespace
+
+extern "C" int ccdk_unpack_b64(const unsigned char *text, int64_t text_bytes, const int64_t *offsets, int32_t n_chips,
+                               int32_t n_obs, int32_t n_pix, int16_t *spectra, uint16_t *qa,
+                               unsigned long long *err, void *stream) {
+    const dim3 grid((unsigned)((n_pix + PIX_T - 1) / PIX_T), (unsigned)((n_obs + OBS_T - 1) / OBS_T),
+                    (unsigned)(n_chips * NLAYER));
+    hipLaunchKernelGGL(ccd_unpack_b64, grid, dim3(256), 0, (hipStream_t)stream, text, text_bytes, offsets, n_obs,
+                       n_pix, spectra, qa, err);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -102,6 +102,8 @@ struct ccdgpu_ctx {
     DevBuf<ccdgpu_segment> pool, csr;
     DevBuf<CcdDetectArgs> args;
     DevBuf<unsigned char> cub_tmp;
+    DevBuf<unsigned char> b64;  // chipmunk payload text of the last ccdgpu_stage_chipmunk
+    DevBuf<int64_t> b64_off;
     std::vector<int64_t> h_offsets;
     ccdgpu_stats last{};
     unsigned long long diag[32] = {};
@@ -120,6 +122,8 @@ struct ccdgpu_ctx {
         csr.release();
         args.release();
         cub_tmp.release();
+        b64.release();
+        b64_off.release();
         for (auto &e : ev)
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
@@ -256,14 +260,17 @@ static int check_params(const ccdgpu_params *p, int32_t n_pix, int32_t n_obs) {
     return 0;
 }
 
-int ccdgpu_stage(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_chips, int32_t n_pix, int32_t n_obs,
-                 const int64_t *dates, const int16_t *spectra, const uint16_t *qa) {
+// Device buffers of a staged batch (inputs, per-slot scratch, outputs) and the dates upload;
+// the pixel data are filled by the caller (a plain upload or the chipmunk decoder).
+static int stage_alloc(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_chips, int32_t n_pix, int32_t n_obs,
+                       const int64_t *dates) {
     if (!c) return fail(CCDGPU_EINVAL, "NULL ctx");
     if (n_chips <= 0) return fail(CCDGPU_EINVAL, "n_chips must be > 0");
     int rc = check_params(params, n_pix, n_obs);
     if (rc) return rc;
-    if (!dates || !spectra || !qa) return fail(CCDGPU_EINVAL, "NULL input buffer");
+    if (!dates) return fail(CCDGPU_EINVAL, "NULL dates");
     HIPCHK(hipSetDevice(c->device));
+    c->staged = false;
     c->params = *params;
     c->n_chips = n_chips;
     c->n_pix = n_pix;
@@ -292,11 +299,67 @@ int ccdgpu_stage(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_chips, in
     if (c->pool_cap < c->total_pix * 8) c->pool_cap = c->total_pix * 8;
     if ((rc = c->pool.ensure(c->pool_cap)) || (rc = c->pool_seq.ensure(c->pool_cap))) return rc;
     HIPCHK(hipMemcpyAsync(c->dates.p, dates, sizeof(int64_t) * nc * no, hipMemcpyHostToDevice, c->stream));
+    return 0;
+}
+
+int ccdgpu_stage(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_chips, int32_t n_pix, int32_t n_obs,
+                 const int64_t *dates, const int16_t *spectra, const uint16_t *qa) {
+    if (!spectra || !qa) return fail(CCDGPU_EINVAL, "NULL input buffer");
+    int rc = stage_alloc(c, params, n_chips, n_pix, n_obs, dates);
+    if (rc) return rc;
+    const size_t nc = (size_t)n_chips, np = (size_t)n_pix, no = (size_t)n_obs;
     HIPCHK(hipMemcpyAsync(c->spectra.p, spectra, sizeof(int16_t) * nc * 7 * np * no, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->qa.p, qa, sizeof(uint16_t) * nc * np * no, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->staged = true;
     c->ran = false;
+    return 0;
+}
+
+int ccdgpu_stage_chipmunk(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_chips, int32_t n_pix, int32_t n_obs,
+                          const int64_t *dates, const char *text, int64_t text_bytes, const int64_t *text_offsets,
+                          double *unpack_seconds) {
+    if (!text || !text_offsets || text_bytes < 0) return fail(CCDGPU_EINVAL, "NULL or empty chipmunk text");
+    if (n_pix <= 0 || n_pix > (1 << 24)) return fail(CCDGPU_EINVAL, "n_pix out of range");
+    // every present payload must lie inside the text (encoded length incl. '=' padding)
+    const int64_t enc = 4 * (((int64_t)2 * n_pix + 2) / 3);
+    const int64_t n_off = (int64_t)n_chips * n_obs * 8;
+    for (int64_t i = 0; i < n_off; ++i) {
+        const int64_t o = text_offsets[i];
+        if (o >= 0 && o + enc > text_bytes)
+            return fail(CCDGPU_EINVAL, "chipmunk payload " + std::to_string(i) + " runs past the end of the text");
+    }
+    int rc = stage_alloc(c, params, n_chips, n_pix, n_obs, dates);
+    if (rc) return rc;
+    if ((rc = c->b64.ensure((size_t)text_bytes + 1)) || (rc = c->b64_off.ensure((size_t)n_off))) return rc;
+    HIPCHK(hipMemcpyAsync(c->b64.p, text, (size_t)text_bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->b64_off.p, text_offsets, sizeof(int64_t) * (size_t)n_off, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemsetAsync(c->counters.p, 0, sizeof(unsigned long long) * 8, c->stream));
+    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    if (ccdk_unpack_b64(c->b64.p, text_bytes, c->b64_off.p, n_chips, n_obs, n_pix, c->spectra.p, c->qa.p,
+                        c->counters.p + 5, c->stream))
+        return fail(CCDGPU_EHIP, std::string("unpack launch: ") + hipGetErrorString(hipGetLastError()));
+    HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    unsigned long long err = 0;
+    HIPCHK(hipMemcpyAsync(&err, c->counters.p + 5, sizeof(err), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[1]);
+    if (unpack_seconds) *unpack_seconds = ms * 1e-3;
+    if (err) return fail(CCDGPU_EINVAL, "chipmunk payload is not valid base64");
+    c->staged = true;
+    c->ran = false;
+    return 0;
+}
+
+int ccdgpu_staged_inputs(ccdgpu_ctx *c, int16_t *spectra, uint16_t *qa) {
+    if (!c || !c->staged) return fail(CCDGPU_EINVAL, "nothing staged");
+    HIPCHK(hipSetDevice(c->device));
+    const size_t nc = (size_t)c->n_chips, np = (size_t)c->n_pix, no = (size_t)c->n_obs;
+    if (spectra)
+        HIPCHK(hipMemcpyAsync(spectra, c->spectra.p, sizeof(int16_t) * nc * 7 * np * no, hipMemcpyDeviceToHost, c->stream));
+    if (qa) HIPCHK(hipMemcpyAsync(qa, c->qa.p, sizeof(uint16_t) * nc * np * no, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
 }
 
