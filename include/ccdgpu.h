@@ -95,6 +95,32 @@ typedef struct ccdgpu_result {
     double seconds_total;       /* wall time of the call                                  */
 } ccdgpu_result;
 
+/* One row of the reference's segment table with its storage types (ccdc/segment.py:16-55,
+ * resources/schema.cql segment; rows of ccdc/pyccd.py:106-148): float columns rounded to
+ * float32 as Spark's FloatType cast does, days as proleptic ordinals (ISO text on the host).
+ * A pixel without change models has one row of pyccd.default (pyccd.py:99-103): days 1/1/1 and
+ * has_model 0, every band / chprob / curqa column null. */
+typedef struct ccdgpu_row {
+    int32_t px, py;                 /* cx + 30 col, cy - 30 row (test/__init__.py:37)          */
+    int32_t sday, eday, bday;
+    int32_t curqa;
+    int32_t has_model;
+    float chprob;
+    float mag[CCDGPU_NBANDS], rmse[CCDGPU_NBANDS];
+    float coef[CCDGPU_NBANDS][7];
+    float intercept[CCDGPU_NBANDS];
+} ccdgpu_row;
+
+/* Segment + pixel table rows of one chip.  Owned by the library until ccdgpu_rows_free. */
+typedef struct ccdgpu_rows {
+    int32_t n_pix, n_obs;
+    int64_t n_rows;
+    int64_t *row_offsets;       /* [n_pix + 1]                                             */
+    ccdgpu_row *rows;           /* [n_rows], pixel-major                                   */
+    int8_t *mask;               /* [n_pix][n_obs] processing mask 0/1, sorted date order   */
+                                /* (pixel table, resources/schema.cql pixel.mask)          */
+} ccdgpu_rows;
+
 typedef struct ccdgpu_ctx ccdgpu_ctx;
 
 const char *ccdgpu_version(void);
@@ -143,6 +169,12 @@ int ccdgpu_stage_chipmunk(ccdgpu_ctx *ctx, const ccdgpu_params *params, int32_t 
  * [n_chips][7][n_pix][n_obs], qa [n_chips][n_pix][n_obs]); either pointer may be NULL. */
 int ccdgpu_staged_inputs(ccdgpu_ctx *ctx, int16_t *spectra, uint16_t *qa);
 int ccdgpu_fetch_staged(ccdgpu_ctx *ctx, int32_t chip, ccdgpu_result *out);
+
+/* Output writer: the segment / pixel table rows of staged chip `chip` of the last run, packed on
+ * the device (ccd_rows.hip) for the chip at (cx, cy) with `width` pixels per chip row (100).
+ * Replaces the per-segment Python formatting of ccdc/pyccd.py:106-148 + Spark's float cast. */
+int ccdgpu_fetch_rows(ccdgpu_ctx *ctx, int32_t chip, int32_t cx, int32_t cy, int32_t width, ccdgpu_rows *out);
+void ccdgpu_rows_free(ccdgpu_rows *out);
 
 /* Kernel statistics of the last run (per launch of the main detection kernel). */
 typedef struct ccdgpu_stats {

@@ -203,6 +203,28 @@ def detect_partition(records, params=None):
     return rows
 
 
+def _run_chips(chips, params, context):
+    """Group chipmunk chips by location, batch locations that share a date vector, stage each
+    batch with the device chip packer and detect it.  Yields (ctx, chip index, (cx, cy),
+    dates [n] int64 descending, n_pix) for every location, batch by batch."""
+    import ccdgpu
+    from ccdc import chipmunk
+    groups = chipmunk.group(chips)
+    ctx = context or ccdgpu.default_context()
+    batches = {}
+    for key, layers in groups.items():
+        d = chipmunk.dates_of(layers)
+        batches.setdefault(d.tobytes(), []).append((key, layers))
+    for members in batches.values():
+        dates, text, offsets = chipmunk.pack_text([layers for _, layers in members])
+        first_payload = next(v for _, layers in members for n in chipmunk.LAYERS for v in layers[n].values())
+        n_pix = chipmunk.payload_pixels(first_payload)
+        ctx.stage_chipmunk(dates, text, offsets, n_pix, params)
+        ctx.run()
+        for c, (key, _) in enumerate(members):
+            yield ctx, c, key, dates[0], n_pix
+
+
 def detect_chips(chips, params=None, context=None):
     """Change detection straight from chipmunk chips (the wire format merlin.create consumes in
     timeseries.rdd, timeseries.py:120): chips of any number of locations, grouped by location,
@@ -213,32 +235,37 @@ def detect_chips(chips, params=None, context=None):
     unsupported QA value, like ccd.detect."""
     import ccdgpu
     from ccdgpu import abi
-    from ccdc import chipmunk, timeseries
-    groups = chipmunk.group(chips)
-    ctx = context or ccdgpu.default_context()
-    batches = {}
-    for key, layers in groups.items():
-        d = chipmunk.dates_of(layers)
-        batches.setdefault(d.tobytes(), []).append((key, layers))
+    from ccdc import timeseries
     rows = {}
-    for members in batches.values():
-        dates, text, offsets = chipmunk.pack_text([layers for _, layers in members])
-        first_payload = next(v for _, layers in members for n in chipmunk.LAYERS for v in layers[n].values())
-        n_pix = chipmunk.payload_pixels(first_payload)
-        ctx.stage_chipmunk(dates, text, offsets, n_pix, params)
-        ctx.run()
-        dlist = [int(x) for x in dates[0]]
-        for c, ((cx, cy), _) in enumerate(members):
-            u = ctx.fetch(c)
-            if u.error_pixel >= 0:
-                err = ccdgpu.QAValueError('unsupported QA value at pixel %d of chip (%d, %d)' % (u.error_pixel, cx, cy))
-                raise err
-            out = []
-            for px, (_, _, ppx, ppy) in enumerate(timeseries.chip_keys(cx, cy, n_pix)):
-                out.extend(format(cx=cx, cy=cy, px=ppx, py=ppy, dates=dlist,
-                                  ccdresult=abi.pixel_result(u, px, ccd.algorithm)))
-            rows[(cx, cy)] = out
-    return [r for key in groups for r in rows[key]]
+    order = []
+    for ctx, c, (cx, cy), dates, n_pix in _run_chips(chips, params, context):
+        u = ctx.fetch(c)
+        if u.error_pixel >= 0:
+            raise ccdgpu.QAValueError('unsupported QA value at pixel %d of chip (%d, %d)' % (u.error_pixel, cx, cy))
+        dlist = [int(x) for x in dates]
+        out = []
+        for px, (_, _, ppx, ppy) in enumerate(timeseries.chip_keys(cx, cy, n_pix)):
+            out.extend(format(cx=cx, cy=cy, px=ppx, py=ppy, dates=dlist,
+                              ccdresult=abi.pixel_result(u, px, ccd.algorithm)))
+        rows[(cx, cy)] = out
+        order.append((cx, cy))
+    return [r for key in order for r in rows[key]]
+
+
+def detect_chips_tables(chips, params=None, context=None, width=100):
+    """Columnar variant of ``detect_chips``: [((cx, cy), {'segment', 'pixel', 'chip'} Arrow
+    tables)] with the reference's column names and storage types (ccdc.sink), the rows packed
+    on the device (ccdgpu.Context.fetch_rows) instead of formatted one dict at a time."""
+    import ccdgpu
+    from ccdc import sink
+    out = []
+    for ctx, c, (cx, cy), dates, n_pix in _run_chips(chips, params, context):
+        u = ctx.fetch(c)  # procedure / QA error check
+        if u.error_pixel >= 0:
+            raise ccdgpu.QAValueError('unsupported QA value at pixel %d of chip (%d, %d)' % (u.error_pixel, cx, cy))
+        off, rows, mask = ctx.fetch_rows(c, cx, cy, width)
+        out.append(((cx, cy), sink.tables(cx, cy, dates, off, rows, mask)))
+    return out
 
 
 def rdd(ctx, timeseries):

@@ -49,13 +49,15 @@ def _declare(L):
                                         c.c_void_p, c.c_char_p, c.c_int64, c.c_void_p,
                                         c.POINTER(c.c_double)]
     L.ccdgpu_staged_inputs.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p]
+    L.ccdgpu_fetch_rows.argtypes = [c.c_void_p, c.c_int32, c.c_int32, c.c_int32, c.c_int32, c.POINTER(abi.Rows)]
+    L.ccdgpu_rows_free.argtypes = [c.POINTER(abi.Rows)]
     L.ccdgpu_run_staged.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
     L.ccdgpu_fetch_staged.argtypes = [c.c_void_p, c.c_int32, c.POINTER(abi.Result)]
     L.ccdgpu_last_stats.argtypes = [c.c_void_p, c.POINTER(abi.Stats)]
     L.ccdgpu_diag_counters.argtypes = [c.c_void_p, c.POINTER(c.c_uint64), c.c_int32]
     for name in ('ccdgpu_init', 'ccdgpu_destroy', 'ccdgpu_device_count', 'ccdgpu_synchronize',
                  'ccdgpu_detect_batch', 'ccdgpu_stage', 'ccdgpu_stage_chipmunk', 'ccdgpu_staged_inputs',
-                 'ccdgpu_run_staged', 'ccdgpu_fetch_staged',
+                 'ccdgpu_run_staged', 'ccdgpu_fetch_staged', 'ccdgpu_fetch_rows', 'ccdgpu_rows_free', 'ccdgpu_fetch_rows',
                  'ccdgpu_last_stats', 'ccdgpu_diag_counters'):
         getattr(L, name).restype = c.c_int
     return L
@@ -64,7 +66,7 @@ def _declare(L):
 EXPORTS = ('ccdgpu_version', 'ccdgpu_last_error', 'ccdgpu_params_default', 'ccdgpu_init',
            'ccdgpu_destroy', 'ccdgpu_device_count', 'ccdgpu_synchronize', 'ccdgpu_detect_batch',
            'ccdgpu_result_free', 'ccdgpu_stage', 'ccdgpu_stage_chipmunk', 'ccdgpu_staged_inputs',
-           'ccdgpu_run_staged', 'ccdgpu_fetch_staged',
+           'ccdgpu_run_staged', 'ccdgpu_fetch_staged', 'ccdgpu_fetch_rows', 'ccdgpu_rows_free',
            'ccdgpu_last_stats', 'ccdgpu_diag_counters')
 
 
@@ -218,6 +220,17 @@ class Context(object):
             return abi.unpack(res)
         finally:
             lib().ccdgpu_result_free(ctypes.byref(res))
+
+    def fetch_rows(self, chip, cx, cy, width=100):
+        """Segment / pixel table rows of staged chip ``chip`` (output writer, packed on the
+        device): (row_offsets [n_pix+1], rows abi.ROW_DTYPE [n_rows], mask int8 [n_pix][n_obs])."""
+        r = abi.Rows()
+        rc = lib().ccdgpu_fetch_rows(self._ctx, int(chip), int(cx), int(cy), int(width), ctypes.byref(r))
+        try:
+            _check(rc)
+            return abi.unpack_rows(r)
+        finally:
+            lib().ccdgpu_rows_free(ctypes.byref(r))
 
     def diag_counters(self):
         buf = (ctypes.c_uint64 * 32)()

@@ -57,6 +57,44 @@ SEGMENT_DTYPE = np.dtype([
 assert SEGMENT_DTYPE.itemsize == ctypes.sizeof(Segment)
 
 
+class Row(ctypes.Structure):
+    _fields_ = [
+        ('px', _i32), ('py', _i32), ('sday', _i32), ('eday', _i32), ('bday', _i32),
+        ('curqa', _i32), ('has_model', _i32), ('chprob', ctypes.c_float),
+        ('mag', ctypes.c_float * NBANDS), ('rmse', ctypes.c_float * NBANDS),
+        ('coef', (ctypes.c_float * 7) * NBANDS), ('intercept', ctypes.c_float * NBANDS),
+    ]
+
+
+ROW_DTYPE = np.dtype([
+    ('px', '<i4'), ('py', '<i4'), ('sday', '<i4'), ('eday', '<i4'), ('bday', '<i4'),
+    ('curqa', '<i4'), ('has_model', '<i4'), ('chprob', '<f4'),
+    ('mag', '<f4', (NBANDS,)), ('rmse', '<f4', (NBANDS,)), ('coef', '<f4', (NBANDS, 7)),
+    ('intercept', '<f4', (NBANDS,)),
+])
+assert ROW_DTYPE.itemsize == ctypes.sizeof(Row)
+
+
+class Rows(ctypes.Structure):
+    _fields_ = [
+        ('n_pix', _i32), ('n_obs', _i32), ('n_rows', ctypes.c_int64),
+        ('row_offsets', ctypes.POINTER(ctypes.c_int64)),
+        ('rows', ctypes.POINTER(Row)),
+        ('mask', ctypes.POINTER(ctypes.c_int8)),
+    ]
+
+
+def unpack_rows(r):
+    """ccdgpu_rows -> (row_offsets [n_pix+1], rows ROW_DTYPE [n_rows], mask int8 [n_pix][n_obs]),
+    copied out of library memory."""
+    n_pix, n_obs, n = r.n_pix, r.n_obs, r.n_rows
+    off = np.ctypeslib.as_array(r.row_offsets, shape=(n_pix + 1,)).copy()
+    rows = np.frombuffer(ctypes.string_at(ctypes.cast(r.rows, ctypes.c_void_p), n * ROW_DTYPE.itemsize),
+                         dtype=ROW_DTYPE).copy() if n else np.zeros(0, ROW_DTYPE)
+    mask = np.ctypeslib.as_array(r.mask, shape=(n_pix, n_obs)).copy()
+    return off, rows, mask
+
+
 class Result(ctypes.Structure):
     _fields_ = [
         ('n_pix', _i32), ('n_obs', _i32), ('n_seg', ctypes.c_int64),

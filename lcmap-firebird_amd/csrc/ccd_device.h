@@ -73,6 +73,10 @@ int ccdk_occupancy(int variant, int32_t n_obs);
 int ccdk_unpack_b64(const unsigned char *text, int64_t text_bytes, const int64_t *offsets, int32_t n_chips,
                     int32_t n_obs, int32_t n_pix, int16_t *spectra, uint16_t *qa, unsigned long long *err,
                     void *stream);
+// detection results -> segment / pixel table rows (ccd_rows.hip)
+int ccdk_pack_rows(const ccdgpu_segment *seg, const int64_t *seg_off, const int64_t *row_off, const uint32_t *mask_bits,
+                   int32_t mask_words, int32_t n_pix, int32_t n_obs, int32_t cx, int32_t cy, int32_t width,
+                   ccdgpu_row *rows, int8_t *mask, void *stream);
 int ccdk_scatter(const ccdgpu_segment *pool, const int32_t *pool_seq, int64_t n_pool,
                  const int64_t *offsets, int32_t n_pix_per_chip, ccdgpu_segment *out, void *stream);
 #ifdef __cplusplus

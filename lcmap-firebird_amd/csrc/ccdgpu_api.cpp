@@ -102,6 +102,9 @@ struct ccdgpu_ctx {
     DevBuf<ccdgpu_segment> pool, csr;
     DevBuf<CcdDetectArgs> args;
     DevBuf<unsigned char> cub_tmp;
+    DevBuf<ccdgpu_row> rows;    // output writer scratch (ccdgpu_fetch_rows)
+    DevBuf<int64_t> row_off, seg_off1;
+    DevBuf<int8_t> mask8;
     DevBuf<unsigned char> b64;  // chipmunk payload text of the last ccdgpu_stage_chipmunk
     DevBuf<int64_t> b64_off;
     std::vector<int64_t> h_offsets;
@@ -124,6 +127,10 @@ struct ccdgpu_ctx {
         cub_tmp.release();
         b64.release();
         b64_off.release();
+        rows.release();
+        row_off.release();
+        seg_off1.release();
+        mask8.release();
         for (auto &e : ev)
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
@@ -516,6 +523,56 @@ static int fetch_chip(ccdgpu_ctx *c, int32_t chip, ccdgpu_result *out) {
             break;
         }
     return 0;
+}
+
+int ccdgpu_fetch_rows(ccdgpu_ctx *c, int32_t chip, int32_t cx, int32_t cy, int32_t width, ccdgpu_rows *out) {
+    if (!c || !out) return fail(CCDGPU_EINVAL, "NULL argument");
+    std::memset(out, 0, sizeof(*out));
+    if (!c->ran) return fail(CCDGPU_EINVAL, "no completed run to fetch");
+    if (chip < 0 || chip >= c->n_chips) return fail(CCDGPU_EINVAL, "chip index out of range");
+    if (width <= 0) return fail(CCDGPU_EINVAL, "width must be > 0");
+    HIPCHK(hipSetDevice(c->device));
+    const int np = c->n_pix, no = c->n_obs;
+    const int64_t p0 = (int64_t)chip * np;
+    const int64_t s0 = c->h_offsets[p0];
+    // rows per pixel = max(1, segments): host prefix over the segment offsets already here
+    std::vector<int64_t> soff(np + 1), roff(np + 1);
+    roff[0] = 0;
+    for (int i = 0; i <= np; ++i) soff[i] = c->h_offsets[p0 + i] - s0;
+    for (int i = 0; i < np; ++i) roff[i + 1] = roff[i] + std::max<int64_t>(1, soff[i + 1] - soff[i]);
+    const int64_t n_rows = roff[np];
+    int rc;
+    if ((rc = c->rows.ensure((size_t)n_rows)) || (rc = c->row_off.ensure(np + 1)) || (rc = c->seg_off1.ensure(np + 1)) ||
+        (rc = c->mask8.ensure((size_t)np * no)))
+        return rc;
+    HIPCHK(hipMemcpyAsync(c->seg_off1.p, soff.data(), sizeof(int64_t) * (np + 1), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->row_off.p, roff.data(), sizeof(int64_t) * (np + 1), hipMemcpyHostToDevice, c->stream));
+    if (ccdk_pack_rows(c->csr.p + s0, c->seg_off1.p, c->row_off.p, c->mask.p + (size_t)p0 * c->mask_words, c->mask_words,
+                       np, no, cx, cy, width, c->rows.p, c->mask8.p, c->stream))
+        return fail(CCDGPU_EHIP, "row packing launch failed");
+    out->n_pix = np;
+    out->n_obs = no;
+    out->n_rows = n_rows;
+    out->row_offsets = (int64_t *)std::malloc(sizeof(int64_t) * (np + 1));
+    out->rows = (ccdgpu_row *)std::malloc(sizeof(ccdgpu_row) * (size_t)n_rows);
+    out->mask = (int8_t *)std::malloc((size_t)np * no);
+    if (!out->row_offsets || !out->rows || !out->mask) {
+        ccdgpu_rows_free(out);
+        return fail(CCDGPU_ENOMEM, "host allocation failed");
+    }
+    std::memcpy(out->row_offsets, roff.data(), sizeof(int64_t) * (np + 1));
+    HIPCHK(hipMemcpyAsync(out->rows, c->rows.p, sizeof(ccdgpu_row) * (size_t)n_rows, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(out->mask, c->mask8.p, (size_t)np * no, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+void ccdgpu_rows_free(ccdgpu_rows *r) {
+    if (!r) return;
+    std::free(r->row_offsets);
+    std::free(r->rows);
+    std::free(r->mask);
+    std::memset(r, 0, sizeof(*r));
 }
 
 int ccdgpu_fetch_staged(ccdgpu_ctx *c, int32_t chip, ccdgpu_result *out) {

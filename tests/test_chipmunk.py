@@ -127,3 +127,76 @@ def test_detect_chips_equals_record_path():
     assert len(rows) == len(ref) > 300
     for a, b in zip(rows, ref):
         assert a == b
+
+
+def test_sink_schemas_follow_reference():
+    """Arrow schemas of the sink = the reference Spark schemas (names, order, storage types)."""
+    import pyarrow as pa
+    from ccdc import chip, pixel, pyccd, segment, sink
+    for sch in (pyccd.schema(), segment.schema(), pixel.schema(), chip.schema()):
+        a = sink.arrow_schema(sch)
+        assert a.names == sch.fieldNames()
+        for f, g in zip(sch, a):
+            want = {'int': pa.int32(), 'float': pa.float32(), 'string': pa.string(),
+                    'array<float>': pa.list_(pa.float32()), 'array<string>': pa.list_(pa.string()),
+                    'array<tinyint>': pa.list_(pa.int8())}[f.dataType.simpleString()]
+            assert g.type == want, f.name
+
+
+def test_sink_tables_from_rows_and_default_row(tmp_path):
+    from ccdc import sink
+    from ccdgpu import abi
+    rows = np.zeros(3, abi.ROW_DTYPE)
+    rows['px'], rows['py'] = [30, 30, 60], [0, 0, 0]
+    rows['sday'], rows['eday'], rows['bday'] = [723000, 724000, 1], [723500, 725000, 1], [723600, 725100, 1]
+    rows['has_model'] = [1, 1, 0]
+    rows['chprob'] = [1.0, 0.0, 0.0]
+    rows['curqa'] = [8, 24, 0]
+    rows['coef'][:2] = np.arange(49, dtype=np.float32).reshape(7, 7)
+    off = np.array([0, 2, 3])
+    mask = np.array([[1, 0, 1], [0, 0, 0]], dtype=np.int8)
+    t = sink.tables(0, 0, np.array([723001, 723000, 723010]), off, rows, mask)
+    seg = t['segment'].to_pylist()
+    assert seg[0]['sday'] == '1980-07-04' == __import__('datetime').date.fromordinal(723000).isoformat()
+    assert seg[2]['sday'] == seg[2]['bday'] == '0001-01-01' and seg[2]['blmag'] is None and seg[2]['curqa'] is None
+    assert seg[0]['grcoef'] == [float(x) for x in range(7, 14)] and seg[2]['grcoef'] is None
+    pix = t['pixel'].to_pylist()
+    assert [(p['px'], p['mask']) for p in pix] == [(30, [1, 0, 1]), (60, [0, 0, 0])]
+    assert t['chip'].to_pylist()[0]['dates'][0] == __import__('datetime').date.fromordinal(723001).isoformat()
+    paths = sink.write_parquet(str(tmp_path), t, 0, 0)
+    import pyarrow.parquet as pq
+    assert pq.read_table(paths['segment']).equals(t['segment'])
+
+
+@pytest.mark.gpu
+def test_device_rows_equal_formatted_rows_cast_to_float32():
+    """Output writer: device-packed rows == pyccd.format rows after Spark's float32 cast."""
+    from ccdc import pyccd, sink
+    from ccdgpu import synth
+    d, s, q = synth.chip(synth.config(5), 2, 0, 200)
+    order = np.argsort(d)[::-1]
+    d, s, q = d[order], s[:, :, order], q[:, order]
+    chips = chipmunk.chip_response(-1815585, 1064805, d, s, q)
+    ref = pyccd.detect_chips(chips)
+    (key, t), = pyccd.detect_chips_tables(chips)
+    seg = t['segment'].to_pylist()
+    assert len(seg) == len(ref) > 200
+    f32 = lambda v: None if v is None else float(np.float32(v))
+    for a, b in zip(seg, ref):
+        for k in a:
+            if k == 'rfrawp':
+                assert a[k] is None
+            elif k.endswith('coef'):
+                assert a[k] == (None if b[k] is None else [f32(x) for x in b[k]]), k
+            elif k in ('chprob',) or k.endswith('mag') or k.endswith('rmse') or k.endswith('int'):
+                assert a[k] == f32(b[k]), k
+            else:
+                assert a[k] == b[k], k
+    pix = t['pixel'].to_pylist()
+    first_rows = {}
+    for r in ref:
+        first_rows.setdefault((r['px'], r['py']), r)
+    assert len(pix) == 200
+    for p in pix:
+        assert p['mask'] == [int(x) for x in first_rows[(p['px'], p['py'])]['mask']]
+    assert t['chip'].to_pylist()[0]['dates'] == ref[0]['dates']
