@@ -1586,6 +1586,197 @@ __device__ __forceinline__ void comp_lane(const Px &P, int nf, int dref, double 
 // step x removes x (outlier) or advances past it, and the batch ends at the first step that
 // needs a refit (span test on the last kept observation before it) or detects a change.
 // Removals are applied in one compaction pass per batch.
+// ---- speculative early fits
+// An early lookforward step (no model yet, or fewer than 24 observations in the window) refits
+// the window [a, b) every step, and the next steps' windows are [a, b + 1), [a, b + 2), ... as
+// long as no outlier is removed (removals are rare).  spec_fits fits up to 8 of these windows at
+// once: lane = (window v, band), each lane one whole Lasso (models/lasso.py = sklearn 0.18
+// coordinate descent, gradient form as in cd_lanes) on its own centred Gram held in registers,
+// and its rmse from its own residuals (same arithmetic as resid_at).  The replay in lookforward
+// then walks the steps one by one, installing window v's models when step v needs them.
+constexpr int SPEC_PC = 5;  // design columns of a <= 6-coefficient model (windows < 24 obs)
+struct SpecFit {
+    double w[SPEC_PC];  // coefficients of t, cos wt, sin wt, cos 2wt, sin 2wt
+    double c;           // intercept (original coordinates, sklearn: ym - xm . w)
+    double rmse;
+    int sweeps;
+};
+
+// index of (i, j), i <= j, in a row-major upper triangle of SPEC_PC columns
+__host__ __device__ constexpr int ut(int i, int j) { return i * SPEC_PC - i * (i - 1) / 2 + (j - i); }
+
+__device__ __forceinline__ void spec_fits(Px &P, int a, int nw0, int V, SpecFit &F) {
+    const ccdgpu_params &p = ARGS().p;
+    Lds *L = &LDS();
+    const int l = lane();
+    const int v = l >> 3, band = l & 7;
+    const bool act = band < NB && v < V;
+    const int nv = nw0 + v;       // rows of this lane's window
+    const int R = nw0 + V - 1;    // rows staged (<= 23 < TR)
+    const int t0 = CDR(P, a);
+    const CRow c0 = CROW(P, a);   // value shifts: the window's first observation
+    if (l < R) {
+        const CRow cw = CROW(P, a + l);
+        const GLOBAL_AS double *bs = P.basis + (size_t)cw.ci * CCD_BASIS_STRIDE;
+        double *r = L->row[l];
+        r[0] = bs[0] - (double)t0;
+#pragma unroll
+        for (int c = 1; c < SPEC_PC; ++c) r[c] = bs[c];
+#pragma unroll
+        for (int bd = 0; bd < NB; ++bd) r[8 + bd] = (double)((int)cw.v[bd] - (int)c0.v[bd]);
+    }
+    wsync();
+    const int yb = band < NB ? band : 0;
+    const int y0 = (int)c0.v[yb];
+    // raw sums of the lane's window in shifted coordinates (exact integer shifts)
+    double sx[SPEC_PC], sxy[SPEC_PC], sxx[ut(SPEC_PC - 1, SPEC_PC - 1) + 1];
+    double sy = 0.0, syy = 0.0;
+#pragma unroll
+    for (int i = 0; i < SPEC_PC; ++i) sx[i] = sxy[i] = 0.0;
+#pragma unroll
+    for (int e = 0; e < ut(SPEC_PC - 1, SPEC_PC - 1) + 1; ++e) sxx[e] = 0.0;
+    const int nrow = act ? nv : 0;
+    for (int r = 0; r < nrow; ++r) {
+        const double *row = L->row[r];
+        double x[SPEC_PC];
+#pragma unroll
+        for (int i = 0; i < SPEC_PC; ++i) x[i] = row[i];
+        const double y = row[8 + yb];
+        sy += y;
+        syy += y * y;
+#pragma unroll
+        for (int i = 0; i < SPEC_PC; ++i) {
+            sx[i] += x[i];
+            sxy[i] += x[i] * y;
+#pragma unroll
+            for (int j = i; j < SPEC_PC; ++j) sxx[ut(i, j)] += x[i] * x[j];
+        }
+    }
+    // centred Gram / X'y / y'y (sklearn centres X and y) and the coordinate descent
+    const double n = act ? (double)nv : 1.0;
+    double G[ut(SPEC_PC - 1, SPEC_PC - 1) + 1], q[SPEC_PC];
+#pragma unroll
+    for (int i = 0; i < SPEC_PC; ++i) {
+        q[i] = sxy[i] - sx[i] * (sy / n);
+#pragma unroll
+        for (int j = i; j < SPEC_PC; ++j) G[ut(i, j)] = sxx[ut(i, j)] - sx[i] * (sx[j] / n);
+    }
+    const double yy = syy - sy * (sy / n);
+    const int kc = num_coefs(p, nv);
+    const int pc = kc - 1;
+    const double alpha = p.lasso_alpha * (double)nv;
+    const double tol = p.lasso_tol, tol_s = tol * yy;
+    const int max_iter = p.lasso_max_iter;
+    double rg[SPEC_PC], w[SPEC_PC], g[SPEC_PC];
+    bool can[SPEC_PC];
+#pragma unroll
+    for (int i = 0; i < SPEC_PC; ++i) {
+        const double gd = G[ut(i, i)];
+        rg[i] = gd != 0.0 ? 1.0 / gd : 0.0;
+        can[i] = act && i < pc && gd != 0.0;  // sklearn skips zero-norm columns
+        w[i] = 0.0;
+        g[i] = q[i];
+    }
+    const bool any5 = bal(act && pc > 3) != 0ull;
+    bool done = !act;
+    int sweeps = max_iter;
+    for (int it = 0; it < max_iter; ++it) {
+        if (bal(!done) == 0ull) break;
+        double dmax = 0.0;
+#pragma unroll
+        for (int i = 0; i < SPEC_PC; ++i) {
+            if (i >= 3 && !any5) break;
+            const double tmp = g[i] + G[ut(i, i)] * w[i];
+            const double wn = copysign(fmax(fabs(tmp) - alpha, 0.0), tmp) * rg[i];
+            const bool upd = !done && can[i];
+            const double wnew = upd ? wn : w[i];
+            const double d = wnew - w[i];
+            w[i] = wnew;
+            dmax = fmax(dmax, fabs(d));
+#pragma unroll
+            for (int m = 0; m < SPEC_PC; ++m) g[m] -= G[m < i ? ut(m, i) : ut(i, m)] * d;
+        }
+        double wmax = 0.0;
+#pragma unroll
+        for (int i = 0; i < SPEC_PC; ++i) wmax = fmax(wmax, fabs(w[i]));  // w = 0 past pc
+        const double tw = tol * wmax;
+        const bool near = !done && wmax != 0.0 && (wmax < 1e-280 || (dmax > 0.25 * tw && dmax < 4.0 * tw));
+        bool ratio_lt = dmax <= 0.25 * tw;
+        if (bal(near)) {
+            if (near) ratio_lt = dmax / wmax < tol;
+        }
+        const bool check = !done && (wmax == 0.0 || ratio_lt || it == max_iter - 1);
+        if (bal(check)) {
+            double dual = 0.0, wq = 0.0, wxta = 0.0, l1 = 0.0;
+#pragma unroll
+            for (int i = 0; i < SPEC_PC; ++i) {
+                if (i < pc) dual = fmax(dual, fabs(g[i]));
+                wq += w[i] * q[i];
+                wxta += w[i] * g[i];
+                l1 += fabs(w[i]);
+            }
+            const double ry = yy - wq, rr = ry - wxta;
+            double cst, gap;
+            if (dual > alpha) {
+                cst = alpha / dual;
+                gap = 0.5 * (rr + rr * cst * cst);
+            } else {
+                cst = 1.0;
+                gap = rr;
+            }
+            gap += alpha * l1 - cst * ry;
+            if (check && gap < tol_s) {
+                done = true;
+                sweeps = it + 1;
+            }
+        }
+    }
+    // intercept in original coordinates (means as gram_finalize forms them) and the rmse
+    double dot = (sx[0] + n * (double)t0) / n * w[0];
+#pragma unroll
+    for (int i = 1; i < SPEC_PC; ++i) dot += sx[i] / n * w[i];
+    const double c = (sy + n * (double)y0) / n - dot;
+    double ss = 0.0;
+    for (int r = 0; r < nrow; ++r) {
+        const double *row = L->row[r];
+        double pr = (row[0] + (double)t0) * w[0];
+#pragma unroll
+        for (int i = 1; i < SPEC_PC; ++i) pr += row[i] * w[i];
+        pr += c;
+        const double res = (row[8 + yb] + (double)y0) - pr;
+        ss += res * res;
+    }
+    wsync();  // the row tile is free again (the replay's peek residuals go there)
+#pragma unroll
+    for (int i = 0; i < SPEC_PC; ++i) F.w[i] = w[i];
+    F.c = c;
+    F.rmse = sqrt(ss / (double)(nv - (p.rmse_dof ? kc : 0)));
+    F.sweeps = sweeps;
+}
+
+// Models of speculative window s (lanes (s, band)) into the model slots of LDS; comp = rmse.
+__device__ __forceinline__ void spec_install(Px &P, const SpecFit &F, int s, int nw, int kc) {
+    Lds *L = &LDS();
+    const int l = lane();
+    const int v = l >> 3, band = l & 7;
+    if (v == s && band < NB) {
+#pragma unroll
+        for (int i = 0; i < SPEC_PC; ++i) L->coef[band][i] = F.w[i];
+        L->coef[band][5] = 0.0;
+        L->coef[band][6] = 0.0;
+        L->coef[band][7] = F.c;
+        L->rmse[band] = F.rmse;
+        L->comp[band] = F.rmse;
+        P.sweeps += (unsigned long long)F.sweeps;
+        P.fl_lane += (unsigned long long)F.sweeps * (unsigned long long)(2 * kc * kc + 6 * kc);
+    }
+    P.fits += NB;
+    P.fl += (unsigned long long)nw * (unsigned long long)(kc * (kc + 1) + 14 * kc + 7 * (2 * kc + 3));
+    P.fit_k = 0;  // L->coef no longer describes the accumulated Gram window
+    PH_COUNT(P, 19, 1)
+    wsync();
+}
+
 __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
     const ccdgpu_params &p = ARGS().p;
     Lds *L = &LDS();
@@ -1605,6 +1796,56 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
     for (;;) {
         if (!(b + k < P.m || !have)) break;
         if (!have || b - a < 24) {
+            // early steps: speculative fits of the next windows, then the steps one by one
+            const int nw0 = b - a;
+            int V = 24 - nw0;
+            V = V > 8 ? 8 : V;
+            V = V > P.m - b + 1 ? P.m - b + 1 : V;  // staged rows stay inside the period
+            while (V > 1 && num_coefs(p, nw0 + V - 1) - 1 > SPEC_PC) --V;
+            if (V >= 1 && num_coefs(p, nw0) - 1 <= SPEC_PC) {
+                PH_BEGIN(sf)
+                SpecFit F;
+                spec_fits(P, a, nw0, V, F);
+                PH_END(P, sf, 5)
+                int sp = 0, valid = V - 1, installed = -1;
+                bool brk = false;
+                for (;;) {
+                    if (!(b + k < P.m || !have)) break;
+                    if (have && b - a >= 24) break;
+                    if (sp > valid) break;
+                    nc = num_coefs(p, b - a);
+                    peek_start = b;
+                    fa = a;
+                    fb = b;
+                    fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
+                    if (installed != sp) {
+                        spec_install(P, F, sp, b - a, nc);
+                        installed = sp;
+                    }
+                    nc_fit = nc;
+                    have = true;
+                    double m0;
+                    PH_BEGIN(ep)
+                    const bool chg_now = eval_peek(P, k, b, 1, m0);
+                    PH_END(P, ep, 8)
+                    moff = 0;
+                    if (chg_now) {
+                        change = 1.0;
+                        brk = true;
+                        break;
+                    }
+                    if (m0 > p.outlier_threshold) {
+                        const int rm = b;
+                        compact_drop(P, rm, [&](int j) { return j == rm; });
+                        valid = sp;  // later windows held the removed observation
+                        continue;
+                    }
+                    b += 1;
+                    sp += 1;
+                }
+                if (brk) break;
+                continue;
+            }
             // early step: refit every step, comparison rmse = model rmse
             nc = num_coefs(p, b - a);
             peek_start = b;
