@@ -1377,44 +1377,37 @@ __device__ __forceinline__ void build_closest(const Px &P, int fa, int fb, int k
         L->hist2[w] = (unsigned)s0 | ((unsigned)s1 << 16);  // bin start positions
     }
     wsync();
-    // fill: each add advances the bin's cursor, so afterwards every bin holds its end position
-    for (int i = fa + l; i < fb; i += W) {
-        const int u = u1461(CDR(P, i));
-        const unsigned old = atomicAdd(&L->hist2[u >> 1], 1u << ((u & 1) * 16));
-        const int pos = (int)((old >> ((u & 1) * 16)) & 0xFFFFu);
-        P.bk[gidx(P, pos, P.n, __LINE__)] = (uint16_t)(i - fa);
-    }
-    gsync();
-    // squared residuals in bucket order: lane = bucket position, all 7 bands per lane; their
-    // sums are the models' rmse (lasso.fitted_model) over the same fit window
+    // fill: each add advances the bin's cursor, so afterwards every bin holds its end position.
+    // The same pass writes the observation's squared residuals (current models) at its bucket
+    // position (lane = observation: its row and design loads go out before the LDS atomic);
+    // their sums are the models' rmse (lasso.fitted_model) over the same fit window.
     const Lds *Lc = L;
     double ssq[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) ssq[b] = 0.0;
-    for (int t0 = 0; t0 < nf; t0 += W) {
-        const int t = t0 + l;
-        if (t < nf) {
-            const int j = fa + (int)P.bk[t];
-            const int g = gidx(P, j, P.m, __LINE__);
-            const uint4 q = reinterpret_cast<const uint4 *>(PCR(P))[g];
-            const GLOBAL_AS double *bs = P.basis + (size_t)gidx(P, (int)(q.w >> 16), P.n, __LINE__) * CCD_BASIS_STRIDE;
-            double x[7];
+    for (int i = fa + l; i < fb; i += W) {
+        const uint4 q = reinterpret_cast<const uint4 *>(PCR(P))[gidx(P, i, P.m, __LINE__)];
+        const GLOBAL_AS double *bs = P.basis + (size_t)gidx(P, (int)(q.w >> 16), P.n, __LINE__) * CCD_BASIS_STRIDE;
+        double x[7];
 #pragma unroll
-            for (int c = 0; c < 7; ++c) x[c] = bs[c];
-            const unsigned qw[4] = {q.x, q.y, q.z, q.w};
-            GLOBAL_AS double *o = P.fs + (size_t)t * 8;
+        for (int c = 0; c < 7; ++c) x[c] = bs[c];
+        const int u = u1461(CDR(P, i));
+        const unsigned old = atomicAdd(&L->hist2[u >> 1], 1u << ((u & 1) * 16));
+        const int pos = gidx(P, (int)((old >> ((u & 1) * 16)) & 0xFFFFu), nf, __LINE__);
+        P.bk[pos] = (uint16_t)(i - fa);
+        const unsigned qw[4] = {q.x, q.y, q.z, q.w};
+        GLOBAL_AS double *o = P.fs + (size_t)pos * 8;
 #pragma unroll
-            for (int b = 0; b < NB; ++b) {
-                const double *c = Lc->coef[b];
-                double pr = x[0] * c[0];
+        for (int b = 0; b < NB; ++b) {
+            const double *c = Lc->coef[b];
+            double pr = x[0] * c[0];
 #pragma unroll
-                for (int jj = 1; jj < 7; ++jj) pr += x[jj] * c[jj];
-                pr += c[7];
-                const double y = (double)(int16_t)(qw[b >> 1] >> ((b & 1) * 16));
-                const double r = y - pr;
-                o[b] = r * r;
-                ssq[b] += r * r;
-            }
+            for (int jj = 1; jj < 7; ++jj) pr += x[jj] * c[jj];
+            pr += c[7];
+            const double y = (double)(int16_t)(qw[b >> 1] >> ((b & 1) * 16));
+            const double r = y - pr;
+            o[b] = r * r;
+            ssq[b] += r * r;
         }
     }
     const double den = (double)(nf - (ARGS().p.rmse_dof ? k : 0));
@@ -1548,6 +1541,8 @@ __device__ __forceinline__ void comp_lane(const Px &P, int nf, int dref, double 
 #pragma unroll
     for (int bd = 0; bd < NB; ++bd) cs[bd] = 0.0;
     const int s0 = K > 0 ? bstart(L, (u - K + 1 + 1461) % 1461) : 0;
+    // (unrolled so several rows' loads are in flight; the sum stays in bucket order)
+#pragma unroll 4
     for (int s = 0; s < less; ++s) {
         int pos = s0 + s;
         pos = pos >= nf ? pos - nf : pos;
