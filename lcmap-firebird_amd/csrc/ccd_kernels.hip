@@ -1005,12 +1005,194 @@ __device__ __forceinline__ void tm_trig(const Px &P, int a, int nw, double oc, G
     }
 }
 
+// ---- Tmask for windows of at most 64 observations (the initialize windows): lane = window
+// observation, its design row, value and weights held in registers for the whole call, so the
+// IRLS iterations re-read nothing from memory; the normal equations are summed through the LDS
+// row tile as in tm_normal (same order, same arithmetic: results equal the generic path's).
+__device__ __forceinline__ void tm_normal_reg(const double (&x)[5], double wv, double yv, int nw, int ncol) {
+    Lds *L = &LDS();
+    const int l = lane();
+    int ea = -1, eb = -1;
+    if (l < 15) {
+        int e = l, r = 0;
+        while (e > r) { e -= r + 1; ++r; }
+        ea = r;
+        eb = e;
+    } else if (l < 20) {
+        ea = l - 15;
+        eb = 6;
+    }
+    double acc = 0.0;
+    for (int t0 = 0; t0 < nw; t0 += TR) {
+        const int cnt = nw - t0 < TR ? nw - t0 : TR;
+        if (l >= t0 && l < t0 + cnt) {
+            double *row = L->row[l - t0];
+#pragma unroll
+            for (int r = 0; r < 5; ++r) row[r] = x[r];
+            row[5] = wv;
+            row[6] = yv;
+        }
+        wsync();
+        if (ea >= 0)
+            for (int r = 0; r < cnt; ++r) acc += L->row[r][5] * L->row[r][ea] * L->row[r][eb];
+        wsync();
+    }
+    if (l < 15) {
+        L->G[ea][eb] = acc;
+        L->G[eb][ea] = acc;
+    } else if (l < 20) {
+        L->Q[ea][0] = acc;
+    }
+    wsync();
+    if (ncol == 3 && l == 0) {
+        L->G[3][3] = 1.0;
+        L->G[4][4] = 1.0;
+    }
+    wsync();
+}
+
+__device__ __forceinline__ double tm_dot(const double (&x)[5], const double (&coef)[5]) {
+    double pr = 0.0;
+#pragma unroll
+    for (int r = 0; r < 5; ++r) pr += x[r] * coef[r];
+    return pr;
+}
+
+__device__ __forceinline__ int tmask_reg(Px &P, int a, int b) {
+    const ccdgpu_params &p = ARGS().p;
+    Lds *L = &LDS();
+    const int l = lane();
+    const int nw = b - a;
+    const double w = 2.0 * M_PI / p.avg_days_yr;
+    const double oc = w / ceil(((double)CDR(P, b - 1) - (double)CDR(P, a)) / p.avg_days_yr);
+    const int ncol = (oc == w) ? 3 : 5;
+    const bool in = l < nw;
+    double x[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    uint4 q = {0u, 0u, 0u, 0u};  // the observation's row: band values + sorted index
+    if (in) {
+        q = reinterpret_cast<const uint4 *>(PCR(P))[gidx(P, a + l, P.m, __LINE__)];
+        const GLOBAL_AS double *bs = P.basis + (size_t)gidx(P, (int)(q.w >> 16), P.n, __LINE__) * CCD_BASIS_STRIDE;
+        x[0] = bs[1];
+        x[1] = bs[2];
+        if (ncol == 5) {
+            double sv, cv;
+            sincos(oc * (double)CDR(P, a + l), &sv, &cv);
+            x[2] = cv;
+            x[3] = sv;
+            x[4] = 1.0;
+        } else {
+            x[2] = 1.0;
+        }
+    }
+    if (l < (nw + 31) / 32) L->tflag[l] = 0u;
+    // unweighted normal matrix: OLS solves and leverage h = diag(X (X'X)^-1 X') (robust_fit.RLM)
+    bool ok0;
+    {
+        double G0[5][5], rhs0[5];
+        tm_normal_reg(x, 1.0, 0.0, nw, ncol);
+        tm_load(L, G0, rhs0);
+        ok0 = chol5(G0);
+        if (l == 0)
+#pragma unroll
+            for (int r = 0; r < 5; ++r)
+#pragma unroll
+                for (int c = 0; c < 5; ++c) L->tchol[r][c] = G0[r][c];
+    }
+    wsync();
+    double adj = 0.0;
+    if (in) {
+        double h = 0.9999;
+        if (ok0) {
+            double z[5], hh = 0.0;
+#pragma unroll
+            for (int r = 0; r < 5; ++r) {
+                double s2 = x[r];
+#pragma unroll
+                for (int k = 0; k < r; ++k) s2 -= L->tchol[r][k] * z[k];
+                z[r] = s2 / L->tchol[r][r];
+                hh += z[r] * z[r];
+            }
+            h = hh < 0.9999 ? hh : 0.9999;
+        }
+        adj = 1.0 / sqrt(1.0 - h);
+    }
+    for (int band = 0; band < NB; ++band) {
+        if (!((p.tmask_bands >> band) & 1u)) continue;
+        const unsigned word = (band >> 1) == 0 ? q.x : (band >> 1) == 1 ? q.y : (band >> 1) == 2 ? q.z : q.w;
+        const double yv = in ? (double)(int16_t)(word >> ((band & 1) * 16)) : 0.0;
+        // y statistics (np.std, population)
+        const double ym = wsum(yv) / nw;
+        const double dy = in ? yv - ym : 0.0;
+        const double ystd = sqrt(wsum(dy * dy) / nw);
+        double coef[5], coef0[5];
+        {
+            double Gt[5][5], r0[5];
+            tm_normal_reg(x, 1.0, yv, nw, ncol);
+            tm_load(L, Gt, r0);
+            if (ok0) {
+#pragma unroll
+                for (int r = 0; r < 5; ++r)
+#pragma unroll
+                    for (int c = 0; c < 5; ++c) Gt[r][c] = L->tchol[r][c];
+                chol5_solve(Gt, r0, coef);
+            } else {
+                tm_solve(Gt, r0, coef);
+            }
+        }
+        P.fl += (unsigned long long)nw * 35 + 125;  // OLS fit: n_w 35 + 5^3
+        int iteration = 1;
+        bool converged = false;
+        while (!converged && iteration < 5) {
+#pragma unroll
+            for (int r = 0; r < 5; ++r) coef0[r] = coef[r];
+            const double rr = in ? (yv - tm_dot(x, coef0)) * adj : 0.0;  // signed, adjusted residual
+            // mad = median(sort(|r|)[4:]) / 0.6745: one value per lane, bitonic sort across the wave
+            const int c = nw - 4;
+            const double v = bitonic64(in ? fabs(rr) : __builtin_inf());
+            const double hi = __shfl(v, 4 + c / 2);
+            const double lo = __shfl(v, 4 + (c - 1) / 2);
+            const double med = (c & 1) ? hi : (lo + hi) / 2.0;
+            const double mad = med / 0.6745;
+            const double floor_ = 2.220446049250313e-16 * ystd;
+            const double scale = mad > floor_ ? mad : floor_;
+            const double u = rr / scale;
+            const double qq = u / 4.685;
+            const double om = 1.0 - qq * qq;
+            const double wt = fabs(u) < 4.685 ? om * om : 0.0;
+            double Gw[5][5], rw[5];
+            tm_normal_reg(x, in ? wt : 0.0, yv, nw, ncol);
+            tm_load(L, Gw, rw);
+            tm_solve(Gw, rw, coef);
+            P.fl += (unsigned long long)nw * 35 + 125;  // each IRLS refit: n_w 35 + 5^3
+            iteration += 1;
+            converged = true;
+#pragma unroll
+            for (int r = 0; r < 5; ++r)
+                if (coef[r] - coef0[r] > 1e-8) converged = false;
+        }
+        const double thr = L->vario[band] * p.t_const;
+        const double pr = tm_dot(x, coef) + 0.0;
+        const unsigned long long bm = bal(in && fabs(pr - yv) > thr);
+        if (l == 0) {
+            L->tflag[0] |= (unsigned)bm;
+            if (32 < nw) L->tflag[1] |= (unsigned)(bm >> 32);
+        }
+        wsync();
+    }
+    int cnt = 0;
+    for (int i = l; i < (nw + 31) / 32; i += W) cnt += __popc(L->tflag[i]);
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+    wsync();
+    return cnt;
+}
+
 // Returns the outlier count; outlier flags in L->tflag (bit i = window observation i).
 __device__ __forceinline__ int tmask(Px &P, int a, int b) {
     const ccdgpu_params &p = ARGS().p;
     Lds *L = &LDS();
     const int l = lane();
     const int nw = b - a;
+    if (nw <= W) return tmask_reg(P, a, b);
     const double w = 2.0 * M_PI / p.avg_days_yr;
     const double oc = w / ceil(((double)CDR(P, b - 1) - (double)CDR(P, a)) / p.avg_days_yr);
     const int ncol = (oc == w) ? 3 : 5;
