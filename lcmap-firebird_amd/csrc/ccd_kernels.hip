@@ -39,7 +39,7 @@ constexpr int W = CCD_WAVE;
 constexpr int RW = 16;  // doubles per staged design row: t c1 s1 c2 s2 c3 s3 _ y0..y6 _
 constexpr int TR = 32;  // rows per LDS staging tile
 constexpr int MAXW = CCDGPU_MAX_OBS / 32;
-#define CCD_NPHASE 20
+#define CCD_NPHASE 24
 
 static_assert(TR * RW >= CCDGPU_MAX_PEEK * 8, "row buffer holds the peek residuals");
 // Global-memory pointers kept in the per-pixel state are typed address_space(1) so every access
@@ -151,7 +151,7 @@ static_assert(sizeof(Lds) % 16 == 0, "period rows follow the Lds block 16-byte a
 // (13 ring residuals + 14 per-lane closest-DOY rmse + 15 magnitudes + decisions), 8 single-step
 // peek evaluation, 9 outlier compaction, 10 stability, 11 medians + emit, 12 closest-DOY bucket
 // build; event counts: 16 batched steps executed, 17 batches, 18 single-step peek evaluations,
-// 19 fits.  Per-lane phases (14, 15) are summed in lane 0 only.
+// 19 fits; 20 speculative early fits.  Per-lane phases (14, 15) are summed in lane 0 only.
 #ifdef CCD_PHASE_TIMERS
 // s_memtime returns through lgkmcnt out of order with LDS traffic: drain every counter around
 // each stamp so no LDS result can be consumed early.
@@ -1983,7 +1983,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
                 PH_BEGIN(sf)
                 SpecFit F;
                 spec_fits(P, a, nw0, V, F);
-                PH_END(P, sf, 5)
+                PH_END(P, sf, 20)
                 int sp = 0, valid = V - 1, installed = -1;
                 bool brk = false;
                 for (;;) {

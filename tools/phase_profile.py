@@ -27,6 +27,8 @@ for i, n in enumerate(names):
     out[n] = dc[8 + i] / tot
 for i, n in enumerate(counts):
     out[n] = dc[8 + 16 + i]
+for i, n in enumerate(['spec early fits (CD)']):
+    out[n] = dc[8 + 20 + i] / tot
 out['pixels'] = chips * 10000
 out['cycles_per_pixel'] = tot / out['pixels']
 print(json.dumps(out, indent=1))
