@@ -48,6 +48,7 @@ def parse():
     ap.add_argument('--cpu-threads', type=int, default=16)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-packer', action='store_true', help='skip the chip-packer (chipmunk decode) leg')
+    ap.add_argument('--no-stream', action='store_true', help='skip the end-to-end (PCIe-inclusive) streaming leg')
     return ap.parse_args()
 
 
@@ -177,6 +178,8 @@ def main():
         'prep_ms_per_launch': float(np.mean(prep_ms)),
     }
 
+    if rank == 0 and not args.no_stream:
+        out['end_to_end'] = stream_leg(ctx, D, S, Q)
     if rank == 0 and not args.no_packer:
         out['chip_packer'] = packer_leg(ctx, D[0], S[0], Q[0])
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -187,6 +190,42 @@ def main():
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def stream_leg(ctx, D, S, Q, batches=6):
+    """End-to-end rate from pinned host memory (never ``value``): each batch = the bench's chips,
+    uploaded, detected and its CSR results fetched back.  'sequential' runs upload -> detect ->
+    fetch one after another (pageable ccdgpu_stage); 'overlapped' uploads batch i+1 on the copy
+    stream (ccdgpu_stage_slot, pinned buffers) while batch i is detected."""
+    import ccdgpu
+    n_chips = D.shape[0]
+    pins = []
+    for _ in range(2):
+        arrs = tuple(ccdgpu.pinned_empty(x.shape, x.dtype) for x in (D, S, Q))
+        for dst, src in zip(arrs, (D, S, Q)):
+            dst[...] = src
+        pins.append(arrs)
+    px = n_chips * PIXELS_PER_CHIP * batches
+    t = time.perf_counter()
+    for i in range(batches):
+        ctx.stage(D, S, Q)
+        ctx.run()
+        for c in range(n_chips):
+            ctx.fetch(c)
+    seq = time.perf_counter() - t
+    t = time.perf_counter()
+    ctx.stage_slot(0, *pins[0])
+    for i in range(batches):
+        if i + 1 < batches:
+            ctx.stage_slot((i + 1) & 1, *pins[(i + 1) & 1])
+        ctx.run_slot(i & 1)
+        for c in range(n_chips):
+            ctx.fetch(c)
+    ovl = time.perf_counter() - t
+    return {'unit': 'pixels/s', 'batches': batches, 'chips_per_batch': n_chips,
+            'input_bytes_per_batch': int(D.nbytes + S.nbytes + Q.nbytes),
+            'sequential_pageable': px / seq, 'overlapped_pinned': px / ovl,
+            'note': 'H2D of the inputs + detection + D2H of the CSR results; not the headline value'}
 
 
 def packer_leg(ctx, dates, S, Q):

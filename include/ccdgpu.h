@@ -165,6 +165,19 @@ int ccdgpu_stage_chipmunk(ccdgpu_ctx *ctx, const ccdgpu_params *params, int32_t 
                           int32_t n_obs, const int64_t *dates, const char *text, int64_t text_bytes,
                           const int64_t *text_offsets, double *unpack_seconds);
 
+/* Overlapped upload (HIP copy stream): ccdgpu_stage_slot uploads a batch into input slot 0 or
+ * 1 and returns at once; ccdgpu_run_slot detects the batch of a slot (after its upload) exactly
+ * like ccdgpu_run_staged, results fetched with ccdgpu_fetch_staged / ccdgpu_fetch_rows.  The
+ * streaming loop  stage_slot(0, b0); for i: { stage_slot((i+1)&1, b_{i+1}); run_slot(i&1); fetch }
+ * overlaps each upload with the previous batch's detection.  Host inputs must stay valid and
+ * unchanged until the run_slot of their slot returns; they should be pinned (ccdgpu_host_alloc),
+ * or the upload is synchronous.  Batches of both slots need the same params. */
+int ccdgpu_host_alloc(size_t bytes, void **ptr);
+int ccdgpu_host_free(void *ptr);
+int ccdgpu_stage_slot(ccdgpu_ctx *ctx, int32_t slot, const ccdgpu_params *params, int32_t n_chips, int32_t n_pix,
+                      int32_t n_obs, const int64_t *dates, const int16_t *spectra, const uint16_t *qa);
+int ccdgpu_run_slot(ccdgpu_ctx *ctx, int32_t slot, double *kernel_seconds);
+
 /* Copy the staged pixel inputs back to the host in the ccdgpu_stage layout (spectra
  * [n_chips][7][n_pix][n_obs], qa [n_chips][n_pix][n_obs]); either pointer may be NULL. */
 int ccdgpu_staged_inputs(ccdgpu_ctx *ctx, int16_t *spectra, uint16_t *qa);

@@ -49,6 +49,11 @@ def _declare(L):
                                         c.c_void_p, c.c_char_p, c.c_int64, c.c_void_p,
                                         c.POINTER(c.c_double)]
     L.ccdgpu_staged_inputs.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p]
+    L.ccdgpu_host_alloc.argtypes = [c.c_size_t, c.POINTER(c.c_void_p)]
+    L.ccdgpu_host_free.argtypes = [c.c_void_p]
+    L.ccdgpu_stage_slot.argtypes = [c.c_void_p, c.c_int32, c.POINTER(abi.Params), c.c_int32, c.c_int32, c.c_int32,
+                                    c.c_void_p, c.c_void_p, c.c_void_p]
+    L.ccdgpu_run_slot.argtypes = [c.c_void_p, c.c_int32, c.POINTER(c.c_double)]
     L.ccdgpu_fetch_rows.argtypes = [c.c_void_p, c.c_int32, c.c_int32, c.c_int32, c.c_int32, c.POINTER(abi.Rows)]
     L.ccdgpu_rows_free.argtypes = [c.POINTER(abi.Rows)]
     L.ccdgpu_run_staged.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
@@ -57,7 +62,8 @@ def _declare(L):
     L.ccdgpu_diag_counters.argtypes = [c.c_void_p, c.POINTER(c.c_uint64), c.c_int32]
     for name in ('ccdgpu_init', 'ccdgpu_destroy', 'ccdgpu_device_count', 'ccdgpu_synchronize',
                  'ccdgpu_detect_batch', 'ccdgpu_stage', 'ccdgpu_stage_chipmunk', 'ccdgpu_staged_inputs',
-                 'ccdgpu_run_staged', 'ccdgpu_fetch_staged', 'ccdgpu_fetch_rows', 'ccdgpu_rows_free', 'ccdgpu_fetch_rows',
+                 'ccdgpu_run_staged', 'ccdgpu_fetch_staged', 'ccdgpu_fetch_rows', 'ccdgpu_host_alloc',
+                 'ccdgpu_host_free', 'ccdgpu_stage_slot', 'ccdgpu_run_slot', 'ccdgpu_rows_free', 'ccdgpu_fetch_rows',
                  'ccdgpu_last_stats', 'ccdgpu_diag_counters'):
         getattr(L, name).restype = c.c_int
     return L
@@ -67,6 +73,7 @@ EXPORTS = ('ccdgpu_version', 'ccdgpu_last_error', 'ccdgpu_params_default', 'ccdg
            'ccdgpu_destroy', 'ccdgpu_device_count', 'ccdgpu_synchronize', 'ccdgpu_detect_batch',
            'ccdgpu_result_free', 'ccdgpu_stage', 'ccdgpu_stage_chipmunk', 'ccdgpu_staged_inputs',
            'ccdgpu_run_staged', 'ccdgpu_fetch_staged', 'ccdgpu_fetch_rows', 'ccdgpu_rows_free',
+           'ccdgpu_host_alloc', 'ccdgpu_host_free', 'ccdgpu_stage_slot', 'ccdgpu_run_slot',
            'ccdgpu_last_stats', 'ccdgpu_diag_counters')
 
 
@@ -171,6 +178,30 @@ class Context(object):
         self._keep = (dates, spectra, qa)
         self._n_pix = n_pix
 
+    def stage_slot(self, slot, dates, spectra, qa, params=None):
+        """Upload a batch into input slot 0/1 on the copy stream and return at once (the arrays
+        must stay alive and unchanged until run_slot(slot) returns; pinned arrays from
+        ``pinned_empty`` make the upload overlap a running detection)."""
+        dates, spectra, qa = _as_inputs(dates, spectra, qa)
+        n_chips, n_pix, n_obs = qa.shape
+        p = params if isinstance(params, abi.Params) else abi.params_from_dict(params)
+        _check(lib().ccdgpu_stage_slot(self._ctx, int(slot), ctypes.byref(p), n_chips, n_pix, n_obs,
+                                       dates.ctypes.data, spectra.ctypes.data, qa.ctypes.data))
+        if not hasattr(self, '_slot_keep'):
+            self._slot_keep = {}
+        self._slot_keep[int(slot)] = (dates, spectra, qa)
+
+    def run_slot(self, slot):
+        """Detect the batch of input slot ``slot`` (waits for its upload); fetch / fetch_rows as
+        after run().  Returns the kernel seconds."""
+        secs = ctypes.c_double(0.0)
+        rc = lib().ccdgpu_run_slot(self._ctx, int(slot), ctypes.byref(secs))
+        if rc not in (0, abi.E_QA):
+            _check(rc)
+        self._keep = self._slot_keep.get(int(slot))
+        self._n_pix = self._keep[2].shape[1]
+        return secs.value
+
     def stage_chipmunk(self, dates, text, offsets, n_pix, params=None):
         """Stage chips from the chipmunk wire format (see ccdc.chipmunk.pack_text):
         dates [C][n] int64, text bytes (concatenated base64 payloads), offsets [C][n][8] int64
@@ -241,6 +272,43 @@ class Context(object):
         s = abi.Stats()
         _check(lib().ccdgpu_last_stats(self._ctx, ctypes.byref(s)))
         return {k: getattr(s, k) for k, _ in abi.Stats._fields_}
+
+
+class _Pinned(object):
+    """Owner of one ccdgpu_host_alloc block (freed when the last array view goes away)."""
+    def __init__(self, nbytes):
+        self.ptr = ctypes.c_void_p()
+        _check(lib().ccdgpu_host_alloc(int(nbytes), ctypes.byref(self.ptr)))
+        self.nbytes = int(nbytes)
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                lib().ccdgpu_host_free(self.ptr)
+        except Exception:
+            pass
+
+
+def pinned_empty(shape, dtype):
+    """numpy array in pinned (page-locked) host memory: uploads from it are asynchronous."""
+    dtype = np.dtype(dtype)
+    n = int(np.prod(shape)) * dtype.itemsize
+    owner = _Pinned(n)
+    buf = (ctypes.c_char * max(n, 1)).from_address(owner.ptr.value)
+    arr = np.frombuffer(buf, dtype=dtype, count=int(np.prod(shape))).reshape(shape)
+    return _PinnedArray(arr, owner)
+
+
+class _PinnedArray(np.ndarray):
+    """ndarray view whose base keeps the pinned allocation alive."""
+    def __new__(cls, arr, owner):
+        obj = np.asarray(arr).view(cls)
+        obj._pinned_owner = owner
+        return obj
+
+    def __array_finalize__(self, obj):
+        if obj is not None:
+            self._pinned_owner = getattr(obj, '_pinned_owner', None)
 
 
 _default_ctx = {}

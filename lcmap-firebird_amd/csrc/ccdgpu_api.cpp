@@ -83,6 +83,12 @@ struct ccdgpu_ctx {
     int slots_per_cu = 0;
     int variant = 3;  // detection kernel register budget: 1..3 waves/SIMD (CCDGPU_KERNEL=w1..w3)
     hipStream_t stream = nullptr;
+    hipStream_t copy_stream = nullptr;  // uploads of ccdgpu_stage_slot (overlap a running detection)
+    hipEvent_t uploaded[2] = {nullptr, nullptr};
+    // inputs the next detection reads: the single staged batch, or one of the two upload slots
+    const int64_t *in_dates = nullptr;
+    const int16_t *in_spectra = nullptr;
+    const uint16_t *in_qa = nullptr;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // staged batch
     bool staged = false, ran = false;
@@ -105,6 +111,11 @@ struct ccdgpu_ctx {
     DevBuf<ccdgpu_row> rows;    // output writer scratch (ccdgpu_fetch_rows)
     DevBuf<int64_t> row_off, seg_off1;
     DevBuf<int8_t> mask8;
+    DevBuf<int64_t> slot_dates[2];   // double-buffered inputs (ccdgpu_stage_slot / ccdgpu_run_slot)
+    DevBuf<int16_t> slot_spectra[2];
+    DevBuf<uint16_t> slot_qa[2];
+    int32_t slot_shape[2][3] = {{0, 0, 0}, {0, 0, 0}};
+    bool slot_ready[2] = {false, false};
     DevBuf<unsigned char> b64;  // chipmunk payload text of the last ccdgpu_stage_chipmunk
     DevBuf<int64_t> b64_off;
     std::vector<int64_t> h_offsets;
@@ -127,6 +138,13 @@ struct ccdgpu_ctx {
         cub_tmp.release();
         b64.release();
         b64_off.release();
+        for (int i = 0; i < 2; ++i) {
+            slot_dates[i].release();
+            slot_spectra[i].release();
+            slot_qa[i].release();
+            if (uploaded[i]) (void)hipEventDestroy(uploaded[i]);
+        }
+        if (copy_stream) (void)hipStreamDestroy(copy_stream);
         rows.release();
         row_off.release();
         seg_off1.release();
@@ -224,6 +242,11 @@ int ccdgpu_init(int device, ccdgpu_ctx **out) {
         return fail(CCDGPU_EHIP, "hipStreamCreate failed");
     }
     for (auto &e : c->ev) (void)hipEventCreate(&e);
+    if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return fail(CCDGPU_EHIP, "hipStreamCreate failed");
+    }
+    for (auto &e : c->uploaded) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
     c->slots_per_cu = 16;
     c->variant = ccdk_period_in_lds() ? 1 : 3;
     if (const char *v = std::getenv("CCDGPU_KERNEL")) {
@@ -270,12 +293,11 @@ static int check_params(const ccdgpu_params *p, int32_t n_pix, int32_t n_obs) {
 // Device buffers of a staged batch (inputs, per-slot scratch, outputs) and the dates upload;
 // the pixel data are filled by the caller (a plain upload or the chipmunk decoder).
 static int stage_alloc(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_chips, int32_t n_pix, int32_t n_obs,
-                       const int64_t *dates) {
+                       const int64_t *dates, bool base_inputs = true) {
     if (!c) return fail(CCDGPU_EINVAL, "NULL ctx");
     if (n_chips <= 0) return fail(CCDGPU_EINVAL, "n_chips must be > 0");
     int rc = check_params(params, n_pix, n_obs);
     if (rc) return rc;
-    if (!dates) return fail(CCDGPU_EINVAL, "NULL dates");
     HIPCHK(hipSetDevice(c->device));
     c->staged = false;
     c->params = *params;
@@ -285,8 +307,10 @@ static int stage_alloc(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_chi
     c->mask_words = (n_obs + 31) / 32;
     c->total_pix = (int64_t)n_chips * n_pix;
     const size_t nc = (size_t)n_chips, np = (size_t)n_pix, no = (size_t)n_obs;
-    if ((rc = c->dates.ensure(nc * no)) || (rc = c->spectra.ensure(nc * 7 * np * no)) ||
-        (rc = c->qa.ensure(nc * np * no)) || (rc = c->order.ensure(nc * no)) ||
+    if (base_inputs && ((rc = c->dates.ensure(nc * no)) || (rc = c->spectra.ensure(nc * 7 * np * no)) ||
+                        (rc = c->qa.ensure(nc * np * no))))
+        return rc;
+    if ((rc = c->order.ensure(nc * no)) ||
         (rc = c->sdates.ensure(nc * no)) || (rc = c->basis.ensure(nc * no * CCD_BASIS_STRIDE)) ||
         (rc = c->procedure.ensure(c->total_pix)) || (rc = c->nseg.ensure(c->total_pix)) ||
         (rc = c->probs.ensure(3 * c->total_pix)) || (rc = c->offsets.ensure(c->total_pix + 1)) ||
@@ -305,13 +329,16 @@ static int stage_alloc(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_chi
         return rc;
     if (c->pool_cap < c->total_pix * 8) c->pool_cap = c->total_pix * 8;
     if ((rc = c->pool.ensure(c->pool_cap)) || (rc = c->pool_seq.ensure(c->pool_cap))) return rc;
-    HIPCHK(hipMemcpyAsync(c->dates.p, dates, sizeof(int64_t) * nc * no, hipMemcpyHostToDevice, c->stream));
+    if (dates) HIPCHK(hipMemcpyAsync(c->dates.p, dates, sizeof(int64_t) * nc * no, hipMemcpyHostToDevice, c->stream));
+    c->in_dates = c->dates.p;
+    c->in_spectra = c->spectra.p;
+    c->in_qa = c->qa.p;
     return 0;
 }
 
 int ccdgpu_stage(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_chips, int32_t n_pix, int32_t n_obs,
                  const int64_t *dates, const int16_t *spectra, const uint16_t *qa) {
-    if (!spectra || !qa) return fail(CCDGPU_EINVAL, "NULL input buffer");
+    if (!dates || !spectra || !qa) return fail(CCDGPU_EINVAL, "NULL input buffer");
     int rc = stage_alloc(c, params, n_chips, n_pix, n_obs, dates);
     if (rc) return rc;
     const size_t nc = (size_t)n_chips, np = (size_t)n_pix, no = (size_t)n_obs;
@@ -326,7 +353,7 @@ int ccdgpu_stage(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_chips, in
 int ccdgpu_stage_chipmunk(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_chips, int32_t n_pix, int32_t n_obs,
                           const int64_t *dates, const char *text, int64_t text_bytes, const int64_t *text_offsets,
                           double *unpack_seconds) {
-    if (!text || !text_offsets || text_bytes < 0) return fail(CCDGPU_EINVAL, "NULL or empty chipmunk text");
+    if (!dates || !text || !text_offsets || text_bytes < 0) return fail(CCDGPU_EINVAL, "NULL or empty chipmunk text");
     if (n_pix <= 0 || n_pix > (1 << 24)) return fail(CCDGPU_EINVAL, "n_pix out of range");
     // every present payload must lie inside the text (encoded length incl. '=' padding)
     const int64_t enc = 4 * (((int64_t)2 * n_pix + 2) / 3);
@@ -359,13 +386,72 @@ int ccdgpu_stage_chipmunk(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_
     return 0;
 }
 
+int ccdgpu_host_alloc(size_t bytes, void **ptr) {
+    if (!ptr) return fail(CCDGPU_EINVAL, "NULL ptr");
+    *ptr = nullptr;
+    if (hipHostMalloc(ptr, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+        *ptr = nullptr;
+        return fail(CCDGPU_ENOMEM, "hipHostMalloc failed (" + std::to_string(bytes) + " bytes)");
+    }
+    return 0;
+}
+
+int ccdgpu_host_free(void *ptr) {
+    if (ptr) HIPCHK(hipHostFree(ptr));
+    return 0;
+}
+
+int ccdgpu_stage_slot(ccdgpu_ctx *c, int32_t slot, const ccdgpu_params *params, int32_t n_chips, int32_t n_pix,
+                      int32_t n_obs, const int64_t *dates, const int16_t *spectra, const uint16_t *qa) {
+    if (!c) return fail(CCDGPU_EINVAL, "NULL ctx");
+    if (slot < 0 || slot > 1) return fail(CCDGPU_EINVAL, "slot must be 0 or 1");
+    if (!dates || !spectra || !qa) return fail(CCDGPU_EINVAL, "NULL input buffer");
+    if (n_chips <= 0) return fail(CCDGPU_EINVAL, "n_chips must be > 0");
+    int rc = check_params(params, n_pix, n_obs);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(c->device));
+    const size_t nc = (size_t)n_chips, np = (size_t)n_pix, no = (size_t)n_obs;
+    if ((rc = c->slot_dates[slot].ensure(nc * no)) || (rc = c->slot_spectra[slot].ensure(nc * 7 * np * no)) ||
+        (rc = c->slot_qa[slot].ensure(nc * np * no)))
+        return rc;
+    // the slot's previous batch was detected by a ccdgpu_run_slot that has returned, so the
+    // uploads may overwrite it; they run on the copy stream, concurrent with any detection
+    HIPCHK(hipMemcpyAsync(c->slot_dates[slot].p, dates, sizeof(int64_t) * nc * no, hipMemcpyHostToDevice, c->copy_stream));
+    HIPCHK(hipMemcpyAsync(c->slot_spectra[slot].p, spectra, sizeof(int16_t) * nc * 7 * np * no, hipMemcpyHostToDevice, c->copy_stream));
+    HIPCHK(hipMemcpyAsync(c->slot_qa[slot].p, qa, sizeof(uint16_t) * nc * np * no, hipMemcpyHostToDevice, c->copy_stream));
+    HIPCHK(hipEventRecord(c->uploaded[slot], c->copy_stream));
+    c->slot_shape[slot][0] = n_chips;
+    c->slot_shape[slot][1] = n_pix;
+    c->slot_shape[slot][2] = n_obs;
+    c->slot_ready[slot] = true;
+    c->params = *params;
+    return 0;
+}
+
+int ccdgpu_run_slot(ccdgpu_ctx *c, int32_t slot, double *kernel_seconds) {
+    if (!c) return fail(CCDGPU_EINVAL, "NULL ctx");
+    if (slot < 0 || slot > 1 || !c->slot_ready[slot]) return fail(CCDGPU_EINVAL, "slot has no staged batch");
+    const ccdgpu_params params = c->params;
+    const int32_t *sh = c->slot_shape[slot];
+    int rc = stage_alloc(c, &params, sh[0], sh[1], sh[2], nullptr, false);
+    if (rc) return rc;
+    HIPCHK(hipStreamWaitEvent(c->stream, c->uploaded[slot], 0));
+    c->in_dates = c->slot_dates[slot].p;
+    c->in_spectra = c->slot_spectra[slot].p;
+    c->in_qa = c->slot_qa[slot].p;
+    c->staged = true;
+    c->ran = false;
+    c->slot_ready[slot] = false;
+    return ccdgpu_run_staged(c, kernel_seconds);
+}
+
 int ccdgpu_staged_inputs(ccdgpu_ctx *c, int16_t *spectra, uint16_t *qa) {
     if (!c || !c->staged) return fail(CCDGPU_EINVAL, "nothing staged");
     HIPCHK(hipSetDevice(c->device));
     const size_t nc = (size_t)c->n_chips, np = (size_t)c->n_pix, no = (size_t)c->n_obs;
     if (spectra)
-        HIPCHK(hipMemcpyAsync(spectra, c->spectra.p, sizeof(int16_t) * nc * 7 * np * no, hipMemcpyDeviceToHost, c->stream));
-    if (qa) HIPCHK(hipMemcpyAsync(qa, c->qa.p, sizeof(uint16_t) * nc * np * no, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(spectra, c->in_spectra, sizeof(int16_t) * nc * 7 * np * no, hipMemcpyDeviceToHost, c->stream));
+    if (qa) HIPCHK(hipMemcpyAsync(qa, c->in_qa, sizeof(uint16_t) * nc * np * no, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
 }
@@ -383,8 +469,8 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
     a.mask_words = c->mask_words;
     a.n_slots = c->n_slots;
     a.total_pix = c->total_pix;
-    a.spectra = c->spectra.p;
-    a.qa = c->qa.p;
+    a.spectra = c->in_spectra;
+    a.qa = c->in_qa;
     a.order = c->order.p;
     a.sdates = c->sdates.p;
     a.basis = c->basis.p;
@@ -411,7 +497,7 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         HIPCHK(hipMemsetAsync(c->stats.p, 0, sizeof(unsigned long long) * 32, c->stream));
         if (ccdk_set_args(&a, c->stream)) return fail(CCDGPU_EHIP, "copying kernel arguments to constant memory failed");
         HIPCHK(hipEventRecord(c->ev[0], c->stream));
-        if (ccdk_prep(c->dates.p, c->n_chips, c->n_obs, p.avg_days_yr, c->order.p, c->sdates.p, c->basis.p, c->stream))
+        if (ccdk_prep(c->in_dates, c->n_chips, c->n_obs, p.avg_days_yr, c->order.p, c->sdates.p, c->basis.p, c->stream))
             return fail(CCDGPU_EHIP, std::string("prep launch: ") + hipGetErrorString(hipGetLastError()));
         HIPCHK(hipEventRecord(c->ev[1], c->stream));
         if (ccdk_detect(c->n_slots, c->variant, c->n_obs, c->stream))

@@ -160,3 +160,31 @@ def test_native_library_is_what_ran(ctx):
     ctx.detect_batch(d, s, q)
     maps = open('/proc/self/maps').read()
     assert 'libccdgpu.so' in maps
+
+
+def test_upload_slots_match_staged_path(ctx):
+    """Double-buffered uploads (ccdgpu_stage_slot / ccdgpu_run_slot, copy stream + pinned host
+    memory): each batch's results equal the plain staged path's, with the next batch's upload in
+    flight during a detection."""
+    import ccdgpu as cg
+    batches = []
+    for seed in (1, 2, 3):
+        d, s, q = synth.chip(synth.config(2), seed, 0, 512)
+        pd, ps, pq = cg.pinned_empty(d.shape, d.dtype), cg.pinned_empty(s.shape, s.dtype), cg.pinned_empty(q.shape, q.dtype)
+        pd[...], ps[...], pq[...] = d, s, q
+        batches.append((pd, ps, pq))
+    ref = []
+    for d, s, q in batches:
+        ctx.stage(d[None], s[None], q[None])
+        ctx.run()
+        ref.append(ctx.fetch(0))
+    ctx.stage_slot(0, batches[0][0][None], batches[0][1][None], batches[0][2][None])
+    for i in range(3):
+        if i + 1 < 3:
+            nd, ns, nq = batches[i + 1]
+            ctx.stage_slot((i + 1) & 1, nd[None], ns[None], nq[None])
+        ctx.run_slot(i & 1)
+        got = ctx.fetch(0)
+        assert np.array_equal(got.seg_offsets, ref[i].seg_offsets)
+        assert got.segments.tobytes() == ref[i].segments.tobytes()
+        assert np.array_equal(got.mask, ref[i].mask)
