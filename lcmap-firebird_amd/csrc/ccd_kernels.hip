@@ -155,10 +155,16 @@ static_assert(sizeof(Lds) % 16 == 0, "period rows follow the Lds block 16-byte a
 #ifdef CCD_PHASE_TIMERS
 // s_memtime returns through lgkmcnt out of order with LDS traffic: drain every counter around
 // each stamp so no LDS result can be consumed early.
+// (CCD_PHASE_TIMERS_RAW: no draining -- outstanding memory latency is then charged to the phase
+// that waits for it; closer to the undisturbed schedule of an issue-bound kernel)
 __device__ __forceinline__ unsigned long long ph_stamp() {
+#ifndef CCD_PHASE_TIMERS_RAW
     __builtin_amdgcn_s_waitcnt(0);
+#endif
     const unsigned long long t = __builtin_amdgcn_s_memtime();
+#ifndef CCD_PHASE_TIMERS_RAW
     __builtin_amdgcn_s_waitcnt(0);
+#endif
     return t;
 }
 #define PH_BEGIN(id) const unsigned long long _ph_##id = ph_stamp();
