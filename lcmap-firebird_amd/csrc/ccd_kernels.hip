@@ -531,14 +531,13 @@ template <int J>
 __device__ __forceinline__ double bcast8(double v) {
     constexpr int q = (J & 3) * 0x55;  // quad_perm [J%4, J%4, J%4, J%4]
     const double t = dpp<q>(v);
-    const bool upper = (lane() & 4) != 0;
-    if (J < 4) {
-        const double u = dpp<0x114>(t);  // row_shr:4 -- lane i <- lane i - 4
-        return upper ? u : t;
-    } else {
-        const double u = dpp<0x104>(t);  // row_shl:4 -- lane i <- lane i + 4
-        return upper ? t : u;
-    }
+    // the other quad of each group takes t over from the quad that holds lane J: a DPP move with
+    // a bank mask (banks = quads of a 16-lane row) writes only those lanes and keeps t elsewhere
+    constexpr int ctrl = J < 4 ? 0x114 : 0x104;   // row_shr:4 (lane i <- i - 4) / row_shl:4 (i <- i + 4)
+    constexpr int banks = J < 4 ? 0xA : 0x5;      // quads 1, 3 / quads 0, 2
+    const int lo = __double2loint(t), hi = __double2hiint(t);
+    return __hiloint2double(__builtin_amdgcn_update_dpp(hi, hi, ctrl, 0xF, banks, false),
+                            __builtin_amdgcn_update_dpp(lo, lo, ctrl, 0xF, banks, false));
 }
 
 // One coordinate of the cyclic sweep (coordinate J of every band group).  Lane (b, k) holds
