@@ -525,27 +525,12 @@ __device__ __forceinline__ double gmax8(double v) {
     return fmax(v, dpp<0x141>(v));
 }
 
-// Lane (group base + J) of every 8-lane group, broadcast to the whole group: quad_perm broadcast
-// inside each quad, then row_shr / row_shl 4 carries it to the other quad of the group.
-template <int J>
-__device__ __forceinline__ double bcast8(double v) {
-    constexpr int q = (J & 3) * 0x55;  // quad_perm [J%4, J%4, J%4, J%4]
-    const double t = dpp<q>(v);
-    // the other quad of each group takes t over from the quad that holds lane J: a DPP move with
-    // a bank mask (banks = quads of a 16-lane row) writes only those lanes and keeps t elsewhere
-    constexpr int ctrl = J < 4 ? 0x114 : 0x104;   // row_shr:4 (lane i <- i - 4) / row_shl:4 (i <- i + 4)
-    constexpr int banks = J < 4 ? 0xA : 0x5;      // quads 1, 3 / quads 0, 2
-    const int lo = __double2loint(t), hi = __double2hiint(t);
-    return __hiloint2double(__builtin_amdgcn_update_dpp(hi, hi, ctrl, 0xF, banks, false),
-                            __builtin_amdgcn_update_dpp(lo, lo, ctrl, 0xF, banks, false));
-}
-
 // One coordinate of the cyclic sweep (coordinate J of every band group).  Lane (b, k) holds
 // g_k = q_k - sum_m G_km w_m (the correlation X_k . R of sklearn's residual form); coordinate J's
 // update uses tmp = X_J . (R + w_J X_J) = g_J + G_JJ w_J, then every g_k absorbs the change.
 template <int J>
 __device__ __forceinline__ void cd_coord(int k, bool live, double alpha, double gkk, double rgkk,
-                                         double gcolJ, double &g, double &w) {
+                                         double ngcolJ, double &g, double &w) {
     const double tmp = g + gkk * w;
     // sklearn: fsign(tmp) * fmax(|tmp| - alpha, 0) / norm (a signed zero below alpha, as there)
     const double wn = copysign(fmax(fabs(tmp) - alpha, 0.0), tmp) * rgkk;
@@ -553,7 +538,16 @@ __device__ __forceinline__ void cd_coord(int k, bool live, double alpha, double 
     const double wnew = upd ? wn : w;
     const double d = wnew - w;  // 0 outside the updated lane
     w = wnew;
-    g -= gcolJ * bcast8<J>(d);
+    // g += (-G_kJ) * d_J: two 64-bit DPP FMAs, row_newbcast (lane J of the 16-lane row to the
+    // row) with the bank mask of the band group that owns that lane -- lanes 0-7 of each row take
+    // lane J, lanes 8-15 lane 8 + J.  s_nop 1 before each: a DPP FMA reads its operands (the
+    // accumulator included) 2 wait states behind a VALU write of them -- back to back, the second
+    // FMA loses the first one's result (tools/probe/dpp64.hip, measured on gfx950).
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0x3\n\t"
+        "s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:%4 row_mask:0xf bank_mask:0xc"
+        : "+v"(g) : "v"(d), "v"(ngcolJ), "i"(J), "i"(J + 8));
 }
 
 // sklearn 0.18 enet_coordinate_descent (beta = 0, cyclic, duality-gap stop) in gradient form,
@@ -567,7 +561,7 @@ __device__ __forceinline__ int cd_lanes(Lds *L, int pc, double alpha, int max_it
     const bool act = b < NB && k < pc;
     double gcol[7];
 #pragma unroll
-    for (int j = 0; j < 7; ++j) gcol[j] = (act && j < pc) ? L->G[j][k] : 0.0;
+    for (int j = 0; j < 7; ++j) gcol[j] = (act && j < pc) ? -L->G[j][k] : 0.0;  // negated: g += gcol * d
     const double gkk = act ? L->G[k][k] : 0.0;
     const double rgkk = gkk != 0.0 ? 1.0 / gkk : 0.0;  // w_k = S(tmp, alpha) / G_kk as a multiply
     const double q = act ? L->Q[k][b] : 0.0;
