@@ -555,7 +555,9 @@ __device__ __forceinline__ void cd_coord(int k, bool live, double alpha, double 
 // a coordinate update is broadcast to its band group by DPP and folded into every g (no
 // per-coordinate reduction).  Writes L->coef[b][0..6]; returns the sweep count (every lane of
 // the band's group).
-__device__ __forceinline__ int cd_lanes(Lds *L, int pc, double alpha, int max_iter, double tol) {
+template <int PC>  // active columns as a constant (3, 5, 7: 4, 6, 8 coefficients), 0 = runtime pc
+__device__ __forceinline__ int cd_sweep(Lds *L, int pc_rt, double alpha, int max_iter, double tol) {
+    const int pc = PC ? PC : pc_rt;
     const int l = lane();
     const int b = l >> 3, k = l & 7;
     const bool act = b < NB && k < pc;
@@ -618,6 +620,15 @@ __device__ __forceinline__ int cd_lanes(Lds *L, int pc, double alpha, int max_it
     }
     if (b < NB && k < 7) L->coef[b][k] = act ? w : 0.0;
     return sweeps;
+}
+// the sweep with its coordinate count unrolled for the three model sizes (no per-coordinate branch)
+__device__ __forceinline__ int cd_lanes(Lds *L, int pc, double alpha, int max_iter, double tol) {
+    switch (pc) {
+    case 3: return cd_sweep<3>(L, pc, alpha, max_iter, tol);
+    case 5: return cd_sweep<5>(L, pc, alpha, max_iter, tol);
+    case 7: return cd_sweep<7>(L, pc, alpha, max_iter, tol);
+    default: return cd_sweep<0>(L, pc, alpha, max_iter, tol);
+    }
 }
 
 // residual of band b at compacted observation j for the current models (lasso.predict)
