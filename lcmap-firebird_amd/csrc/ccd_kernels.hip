@@ -518,11 +518,17 @@ __device__ __forceinline__ double gsum8(double v) {
     v += dpp<0x4E>(v);
     return v + dpp<0x141>(v);
 }
-// (fmax: one v_max_f64 per level; every operand here is a non-NaN magnitude)
+// one v_max_f64 per level: every operand here is a non-NaN magnitude, so the sNaN quieting fmax
+// would add (a canonicalising max of each DPP operand) is left out
+__device__ __forceinline__ double vmax(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 __device__ __forceinline__ double gmax8(double v) {
-    v = fmax(v, dpp<0xB1>(v));
-    v = fmax(v, dpp<0x4E>(v));
-    return fmax(v, dpp<0x141>(v));
+    v = vmax(v, dpp<0xB1>(v));
+    v = vmax(v, dpp<0x4E>(v));
+    return vmax(v, dpp<0x141>(v));
 }
 
 // One coordinate of the cyclic sweep (coordinate J of every band group).  Lane (b, k) holds
@@ -531,13 +537,14 @@ __device__ __forceinline__ double gmax8(double v) {
 template <int J>
 __device__ __forceinline__ void cd_coord(int k, bool live, double alpha, double gkk, double rgkk,
                                          double ngcolJ, double &g, double &w) {
-    const double tmp = g + gkk * w;
+#pragma clang fp contract(off)  // d = wn - w rounded as w's own update (no fma with the product)
+    const double tmp = fma(gkk, w, g);
     // sklearn: fsign(tmp) * fmax(|tmp| - alpha, 0) / norm (a signed zero below alpha, as there)
     const double wn = copysign(fmax(fabs(tmp) - alpha, 0.0), tmp) * rgkk;
-    const bool upd = live && k == J;
-    const double wnew = upd ? wn : w;
-    const double d = wnew - w;  // 0 outside the updated lane
-    w = wnew;
+    // d is read from lane J only; a finished group's gcol is zero, so d needs no gating and the
+    // select of w stays off the chain into the FMAs
+    const double d = wn - w;
+    w = (live && k == J) ? wn : w;
     // g += (-G_kJ) * d_J: two 64-bit DPP FMAs, row_newbcast (lane J of the 16-lane row to the
     // row) with the bank mask of the band group that owns that lane -- lanes 0-7 of each row take
     // lane J, lanes 8-15 lane 8 + J.  s_nop 1 before each: a DPP FMA reads its operands (the
@@ -615,6 +622,8 @@ __device__ __forceinline__ int cd_sweep(Lds *L, int pc_rt, double alpha, int max
             if (check && gap < tol_s) {
                 done = true;
                 sweeps = it + 1;
+#pragma unroll
+                for (int j = 0; j < 7; ++j) gcol[j] = 0.0;  // g and w of the group stay as they are
             }
         }
     }
