@@ -1724,8 +1724,9 @@ __device__ __forceinline__ int cnt_within(const Lds *L, int nf, int u, int d) {
 // from the bucket list and bucket-ordered squared residuals build_closest left (nf > 24).
 // Entries at distance < K form one circular run of bucket positions; at distance exactly K the
 // lowest fit-relative indices win (stable argsort).
-__device__ __forceinline__ void comp_lane(const Px &P, int nf, int dref, double (&cs)[NB]) {
+__device__ __forceinline__ void comp_lane(Px &P, int nf, int dref, double (&cs)[NB]) {
     const Lds *L = &LDS();
+    PH_BEGIN(c1)
     const int u = u1461(dref);
     int lo = 0, hi = 730;  // smallest K with cnt_within(K) >= 24
 #pragma unroll
@@ -1742,6 +1743,8 @@ __device__ __forceinline__ void comp_lane(const Px &P, int nf, int dref, double 
 #pragma unroll
     for (int bd = 0; bd < NB; ++bd) cs[bd] = 0.0;
     const int s0 = K > 0 ? bstart(L, (u - K + 1 + 1461) % 1461) : 0;
+    PH_END(P, c1, 21)
+    PH_BEGIN(c2)
     // (unrolled so several rows' loads are in flight; the sum stays in bucket order)
 #pragma unroll 4
     for (int s = 0; s < less; ++s) {
@@ -1751,6 +1754,8 @@ __device__ __forceinline__ void comp_lane(const Px &P, int nf, int dref, double 
 #pragma unroll
         for (int bd = 0; bd < NB; ++bd) cs[bd] += f[bd];
     }
+    PH_END(P, c2, 22)
+    PH_BEGIN(c3)
     const int b1 = (u - K + 1461) % 1461, b2 = (u + K) % 1461;
     const int c1 = bcount(L, b1), c2 = K > 0 ? bcount(L, b2) : 0;
     const int st1 = bstart(L, b1), st2 = bstart(L, b2);
@@ -1771,6 +1776,7 @@ __device__ __forceinline__ void comp_lane(const Px &P, int nf, int dref, double 
     }
 #pragma unroll
     for (int bd = 0; bd < NB; ++bd) cs[bd] = sqrt(cs[bd]) / 4.0;
+    PH_END(P, c3, 23)
 }
 
 // change.lookforward.  The first steps (no model yet, or fewer than 24 observations in the

@@ -27,7 +27,7 @@ for i, n in enumerate(names):
     out[n] = dc[8 + i] / tot
 for i, n in enumerate(counts):
     out[n] = dc[8 + 16 + i]
-for i, n in enumerate(['spec early fits (CD)']):
+for i, n in enumerate(['spec early fits (CD)', 'closest: search', 'closest: run sum', 'closest: ties']):
     out[n] = dc[8 + 20 + i] / tot
 out['pixels'] = chips * 10000
 out['cycles_per_pixel'] = tot / out['pixels']
