@@ -749,51 +749,87 @@ __device__ __forceinline__ void catch_(Px &P, int a, int b, int cqa) {
     emit(P, CDR(P, a), CDR(P, b - 1), bday, b - a, 0.0, cqa, 0.0);
 }
 
-// k-th smallest (0-based) of 16-bit unsigned values produced by gen(i, &v) for i < N (valid if
-// gen returns true): two-pass radix select over 256-bin LDS histograms (L->hist2 as scratch).
-template <class F>
-__device__ __forceinline__ int select_u16(F gen, int N, int k) {
-    Lds *L = &LDS();
+// Bin of the 256-bin histogram L->hist2[0..255] holding the rank-th smallest entry; rank becomes
+// the rank within that bin.
+__device__ __forceinline__ int hist_find(const Lds *L, int &rank) {
     const int l = lane();
-    int hiB = 0, rank = k;
-#pragma unroll 1
-    for (int pass = 0; pass < 2; ++pass) {
-        for (int i = l; i < 256; i += W) L->hist2[i] = 0u;
-        wsync();
-#pragma unroll 4
-        for (int base = 0; base < N; base += W) {
-            const int i = base + l;
-            int v = 0;
-            if (i < N && gen(i, v) && (pass == 0 || (v >> 8) == hiB))
-                atomicAdd(&L->hist2[pass == 0 ? (v >> 8) : (v & 255)], 1u);
+    int carry = 0;
+    for (int b0 = 0; b0 < 256; b0 += W) {
+        const int c = (int)L->hist2[b0 + l];
+        const int cum = wscan_incl(c) + carry;
+        const unsigned long long hit = bal(cum > rank);
+        if (hit) {
+            const int src = __ffsll((long long)hit) - 1;
+            rank -= rdl(cum, src) - rdl(c, src);
+            return b0 + src;
         }
-        wsync();
-        int carry = 0, found = -1;
-        for (int b0 = 0; b0 < 256; b0 += W) {
-            const int c = (int)L->hist2[b0 + l];
-            const int cum = wscan_incl(c) + carry;
-            const unsigned long long hit = bal(cum > rank);
-            if (hit) {
-                const int src = __ffsll((long long)hit) - 1;
-                found = b0 + src;
-                rank -= rdl(cum, src) - rdl(c, src);
-                break;
-            }
-            carry = rdl(cum, W - 1);
-        }
-        wsync();
-        if (pass == 0) hiB = found;
-        else return (hiB << 8) | found;
+        carry = rdl(cum, W - 1);
     }
     return 0;
 }
 
+// Histogram (L->hist2[0..255]) of the low bytes (pass 1, high byte hb) or the high bytes
+// (pass 0, hb < 0) of the values gen produces.
 template <class F>
-__device__ __forceinline__ double median_u16(F gen, int N, int cnt) {
+__device__ __forceinline__ void hist_u16(F gen, int N, int hb) {
+    Lds *L = &LDS();
+    const int l = lane();
+    for (int i = l; i < 256; i += W) L->hist2[i] = 0u;
+    wsync();
+#pragma unroll 4
+    for (int base = 0; base < N; base += W) {
+        const int i = base + l;
+        int v = 0;
+        if (i < N && gen(i, v) && (hb < 0 || (v >> 8) == hb))
+            atomicAdd(&L->hist2[hb < 0 ? (v >> 8) : (v & 255)], 1u);
+    }
+    wsync();
+}
+
+// The k0-th and k1-th smallest (0-based, k0 <= k1) of 16-bit unsigned values produced by
+// gen(i, &v) for i < N: radix select over 256-bin LDS histograms (L->hist2 as scratch), the two
+// ranks sharing every pass whose bin they share.  small_first: when both ranks lie among the
+// values below 256 (counted with ballots, no histogram) the high-byte pass is skipped -- the
+// common case for absolute differences, where a high-byte histogram would put every lane on
+// bin 0.
+template <class F>
+__device__ __forceinline__ void select2_u16(F gen, int N, int k0, int k1, bool small_first, int &v0, int &v1) {
+    Lds *L = &LDS();
+    int h0 = 0, h1 = 0, r0 = k0, r1 = k1;
+    bool known = false;
+    if (small_first) {
+        int c = 0;
+        for (int base = 0; base < N; base += W) {
+            const int i = base + lane();
+            int v = 0;
+            c += popc(bal(i < N && gen(i, v) && v < 256));
+        }
+        known = k1 < c;
+    }
+    if (!known) {
+        hist_u16(gen, N, -1);
+        h0 = hist_find(L, r0);
+        h1 = hist_find(L, r1);
+        wsync();
+    }
+    hist_u16(gen, N, h0);
+    v0 = (h0 << 8) | hist_find(L, r0);
+    if (h1 == h0) {
+        v1 = (h1 << 8) | hist_find(L, r1);
+    } else {
+        wsync();
+        hist_u16(gen, N, h1);
+        v1 = (h1 << 8) | hist_find(L, r1);
+    }
+    wsync();
+}
+
+template <class F>
+__device__ __forceinline__ double median_u16(F gen, int N, int cnt, bool small_first = false) {
     if (cnt <= 0) return __builtin_nan("");
-    if (cnt & 1) return (double)select_u16(gen, N, cnt / 2);
-    const int a = select_u16(gen, N, cnt / 2 - 1);
-    const int b = select_u16(gen, N, cnt / 2);
+    int a, b;
+    select2_u16(gen, N, (cnt - 1) / 2, cnt / 2, small_first, a, b);
+    if (cnt & 1) return (double)a;
     return ((double)a + (double)b) / 2.0;
 }
 
@@ -853,7 +889,7 @@ __device__ __forceinline__ void variogram(Px &P) {
             val = (int)col[i];
             return true;
         };
-        const double med = median_u16(gen, cnt, cnt);
+        const double med = median_u16(gen, cnt, cnt, true);
         if (l == 0) L->vario[band] = med;
         P.fl += 2ull * (unsigned long long)(m - kk);  // 2 per difference per band
     }
@@ -870,7 +906,7 @@ __device__ __forceinline__ void adjust_peek(Px &P) {
         return true;
     };
     const bool narrow = CDR(P, P.m - 1) - CDR(P, 0) <= 65535;  // every gap fits 16 bits
-    const double delta = narrow ? median_u16(gen, P.m - 1, P.m - 1) : median_int(gen, P.m - 1, P.m - 1, 0, 1 << 30);
+    const double delta = narrow ? median_u16(gen, P.m - 1, P.m - 1, true) : median_int(gen, P.m - 1, P.m - 1, 0, 1 << 30);
     const double adj = rint((double)(p.peek_size * 16) / delta);
     if (adj > (double)p.peek_size) {
         P.peek = adj > (double)CCDGPU_MAX_PEEK ? CCDGPU_MAX_PEEK : (int)adj;
