@@ -202,8 +202,8 @@ typedef struct ccdgpu_stats {
 } ccdgpu_stats;
 int ccdgpu_last_stats(ccdgpu_ctx *ctx, ccdgpu_stats *stats);
 
-/* Raw device counters of the last run: [0] band fits, [1] CD sweeps, [2] counted flops,
- * [8 + k] phase-k cycle totals (only in the diagnostic build lib/libccdgpu_diag.so). */
+/* Raw device counters of the last run (up to 48 words): [0] band fits, [1] CD sweeps, [2] counted
+ * flops, [8 + k] phase-k cycle totals (only in the diagnostic build lib/libccdgpu_diag.so). */
 int ccdgpu_diag_counters(ccdgpu_ctx *ctx, uint64_t *out, int32_t n);
 
 #ifdef __cplusplus

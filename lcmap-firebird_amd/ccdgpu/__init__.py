@@ -264,8 +264,8 @@ class Context(object):
             lib().ccdgpu_rows_free(ctypes.byref(r))
 
     def diag_counters(self):
-        buf = (ctypes.c_uint64 * 32)()
-        _check(lib().ccdgpu_diag_counters(self._ctx, buf, 32))
+        buf = (ctypes.c_uint64 * 48)()
+        _check(lib().ccdgpu_diag_counters(self._ctx, buf, 48))
         return list(buf)
 
     def stats(self):

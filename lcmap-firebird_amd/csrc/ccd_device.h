@@ -17,6 +17,8 @@
 
 #include "../../include/ccdgpu.h"
 
+// launch statistics words: 8 counters + CCD_NSTATS - 8 diagnostic phase slots
+#define CCD_NSTATS 48
 #define CCD_NB 7
 #define CCD_WAVE 64
 #define CCD_BASIS_STRIDE 8

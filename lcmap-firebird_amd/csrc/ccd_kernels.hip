@@ -39,7 +39,7 @@ constexpr int W = CCD_WAVE;
 constexpr int RW = 16;  // doubles per staged design row: t c1 s1 c2 s2 c3 s3 _ y0..y6 _
 constexpr int TR = 32;  // rows per LDS staging tile
 constexpr int MAXW = CCDGPU_MAX_OBS / 32;
-#define CCD_NPHASE 24
+#define CCD_NPHASE (CCD_NSTATS - 8)
 
 static_assert(TR * RW >= CCDGPU_MAX_PEEK * 8, "row buffer holds the peek residuals");
 // Global-memory pointers kept in the per-pixel state are typed address_space(1) so every access
@@ -2187,6 +2187,10 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
         P.fl += (unsigned long long)ne *
                 ((unsigned long long)k * (7 * 2 * 8 + 5 * 3) + (unsigned long long)nf * 6 + 5 * 48);
         PH_COUNT(P, 16, ne)
+        PH_COUNT(P, 24, ne <= 16 ? 1 : 0)
+        PH_COUNT(P, 25, ne <= 32 ? 1 : 0)
+        PH_COUNT(P, 26, nv)
+        PH_COUNT(P, 27, Tm ? 0 : 1)
         PH_END(P, cl, 7)
         const unsigned long long rem = xs >= 64 ? O : (O & ((1ull << xs) - 1ull));
         const int R = popc(rem);

@@ -120,7 +120,7 @@ struct ccdgpu_ctx {
     DevBuf<int64_t> b64_off;
     std::vector<int64_t> h_offsets;
     ccdgpu_stats last{};
-    unsigned long long diag[32] = {};
+    unsigned long long diag[CCD_NSTATS] = {};
     ~ccdgpu_ctx() {
         for (auto *b : {&dates, &sdates, &offsets}) b->release();
         spectra.release();
@@ -315,7 +315,7 @@ static int stage_alloc(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_chi
         (rc = c->procedure.ensure(c->total_pix)) || (rc = c->nseg.ensure(c->total_pix)) ||
         (rc = c->probs.ensure(3 * c->total_pix)) || (rc = c->offsets.ensure(c->total_pix + 1)) ||
         (rc = c->mask.ensure((size_t)c->total_pix * c->mask_words)) || (rc = c->counters.ensure(8)) ||
-        (rc = c->stats.ensure(32)) || (rc = c->args.ensure(1)))
+        (rc = c->stats.ensure(CCD_NSTATS)) || (rc = c->args.ensure(1)))
         return rc;
     // persistent grid: one wave slot per resident wave (LDS / register occupancy), capped by
     // CCDGPU_SLOTS_PER_CU
@@ -494,7 +494,7 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         a.pool_cap = c->pool_cap;
         unsigned long long init[8] = {0ull, 0ull, ~0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
         HIPCHK(hipMemcpyAsync(c->counters.p, init, sizeof(init), hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipMemsetAsync(c->stats.p, 0, sizeof(unsigned long long) * 32, c->stream));
+        HIPCHK(hipMemsetAsync(c->stats.p, 0, sizeof(unsigned long long) * CCD_NSTATS, c->stream));
         if (ccdk_set_args(&a, c->stream)) return fail(CCDGPU_EHIP, "copying kernel arguments to constant memory failed");
         HIPCHK(hipEventRecord(c->ev[0], c->stream));
         if (ccdk_prep(c->in_dates, c->n_chips, c->n_obs, p.avg_days_yr, c->order.p, c->sdates.p, c->basis.p, c->stream))
@@ -517,9 +517,9 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         float ms_prep = 0.f, ms_det = 0.f;
         (void)hipEventElapsedTime(&ms_prep, c->ev[0], c->ev[1]);
         (void)hipEventElapsedTime(&ms_det, c->ev[1], c->ev[2]);
-        unsigned long long st[32];
+        unsigned long long st[CCD_NSTATS];
         HIPCHK(hipMemcpy(st, c->stats.p, sizeof(st), hipMemcpyDeviceToHost));
-        for (int i = 0; i < 32; ++i) c->diag[i] = st[i];
+        for (int i = 0; i < CCD_NSTATS; ++i) c->diag[i] = st[i];
         // CSR: exclusive scan of per-pixel counts, then scatter the pool
         int rc;
         if ((rc = c->csr.ensure(c->n_pool > 0 ? c->n_pool : 1))) return rc;
@@ -559,7 +559,7 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
 
 int ccdgpu_diag_counters(ccdgpu_ctx *c, uint64_t *out, int32_t n) {
     if (!c || !out || n < 0) return fail(CCDGPU_EINVAL, "bad argument");
-    for (int i = 0; i < n && i < 32; ++i) out[i] = c->diag[i];
+    for (int i = 0; i < n && i < CCD_NSTATS; ++i) out[i] = c->diag[i];
     return 0;
 }
 
