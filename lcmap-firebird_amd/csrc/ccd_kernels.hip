@@ -768,6 +768,25 @@ __device__ __forceinline__ int hist_find(const Lds *L, int &rank) {
     return 0;
 }
 
+// hist_find over a 256-bin histogram of u16 counters packed two per word.
+__device__ __forceinline__ int hist_find16(const uint32_t *h, int &rank) {
+    const int l = lane();
+    int carry = 0;
+    for (int b0 = 0; b0 < 256; b0 += W) {
+        const int x = b0 + l;
+        const int c = (int)((h[x >> 1] >> ((x & 1) * 16)) & 0xFFFFu);
+        const int cum = wscan_incl(c) + carry;
+        const unsigned long long hit = bal(cum > rank);
+        if (hit) {
+            const int src = __ffsll((long long)hit) - 1;
+            rank -= rdl(cum, src) - rdl(c, src);
+            return b0 + src;
+        }
+        carry = rdl(cum, W - 1);
+    }
+    return 0;
+}
+
 // Histogram (L->hist2[0..255]) of the low bytes (pass 1, high byte hb) or the high bytes
 // (pass 0, hb < 0) of the values gen produces.
 template <class F>
@@ -855,10 +874,18 @@ __device__ __forceinline__ void variogram(Px &P) {
     const int kk = lag ? lag : 1;
     const bool all = lag == 0;
     // the qualifying absolute differences of all 7 bands, compacted once into the slot's scratch
-    // (band-major u16 [7][n]); the 7 medians then read them coalesced
+    // (band-major u16 [7][n]); the same pass histograms every band's differences below 256 in
+    // LDS (u16 counters, 128 words per band, in the row tile) and counts them, so a band whose two
+    // middle ranks lie below 256 -- nearly always -- needs no further pass over its differences
     GLOBAL_AS uint16_t *dv = reinterpret_cast<GLOBAL_AS uint16_t *>(P.fs);
+    uint32_t *h16w = reinterpret_cast<uint32_t *>(&L->row[0][0]);
+    for (int i = l; i < NB * 128; i += W) h16w[i] = 0u;
+    wsync();
     const int stride = P.n;
     int cnt = 0;
+    int small[NB];
+#pragma unroll
+    for (int band = 0; band < NB; ++band) small[band] = 0;
     for (int base = 0; base < m - kk; base += W) {
         const int i = base + l;
         bool ok = false;
@@ -869,27 +896,39 @@ __device__ __forceinline__ void variogram(Px &P) {
             r1 = reinterpret_cast<const uint4 *>(PCR(P))[i + kk];
         }
         const unsigned long long km = bal(ok);
-        if (ok) {
-            const int pos = cnt + below(km);
-            const unsigned a0[4] = {r0.x, r0.y, r0.z, r0.w}, a1[4] = {r1.x, r1.y, r1.z, r1.w};
+        const unsigned a0[4] = {r0.x, r0.y, r0.z, r0.w}, a1[4] = {r1.x, r1.y, r1.z, r1.w};
 #pragma unroll
-            for (int band = 0; band < NB; ++band) {
-                const int v0 = (int)(int16_t)(a0[band >> 1] >> ((band & 1) * 16));
-                const int v1 = (int)(int16_t)(a1[band >> 1] >> ((band & 1) * 16));
-                const int d = v1 - v0;
-                dv[band * stride + pos] = (uint16_t)(d < 0 ? -d : d);
-            }
+        for (int band = 0; band < NB; ++band) {
+            const int v0 = (int)(int16_t)(a0[band >> 1] >> ((band & 1) * 16));
+            const int v1 = (int)(int16_t)(a1[band >> 1] >> ((band & 1) * 16));
+            const int d = v1 - v0;
+            const int ad = d < 0 ? -d : d;
+            const bool lo = ok && ad < 256;
+            small[band] += popc(bal(lo));
+            if (ok) dv[band * stride + cnt + below(km)] = (uint16_t)ad;
+            if (lo) atomicAdd(&h16w[band * 128 + (ad >> 1)], 1u << ((ad & 1) * 16));
         }
         cnt += popc(km);
     }
     gsync();
     for (int band = 0; band < NB; ++band) {
-        const GLOBAL_AS uint16_t *col = dv + band * stride;
-        auto gen = [&](int i, int &val) -> bool {
-            val = (int)col[i];
-            return true;
-        };
-        const double med = median_u16(gen, cnt, cnt, true);
+        double med;
+        if (cnt <= 0) {
+            med = __builtin_nan("");
+        } else if (cnt / 2 < small[band]) {
+            // both middle ranks among the differences below 256: read them off the histogram
+            int r0 = (cnt - 1) / 2, r1 = cnt / 2;
+            const int a = hist_find16(h16w + band * 128, r0);
+            const int b2 = hist_find16(h16w + band * 128, r1);
+            med = (cnt & 1) ? (double)a : ((double)a + (double)b2) / 2.0;
+        } else {
+            const GLOBAL_AS uint16_t *col = dv + band * stride;
+            auto gen = [&](int i, int &val) -> bool {
+                val = (int)col[i];
+                return true;
+            };
+            med = median_u16(gen, cnt, cnt, true);
+        }
         if (l == 0) L->vario[band] = med;
         P.fl += 2ull * (unsigned long long)(m - kk);  // 2 per difference per band
     }
