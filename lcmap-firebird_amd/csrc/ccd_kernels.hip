@@ -675,6 +675,18 @@ __device__ __forceinline__ void fit_models(Px &P, int a, int b, int k, bool with
         P.sweeps += (unsigned long long)sw;  // per-lane; reduced at the end
         P.fl_lane += (unsigned long long)sw * (unsigned long long)(2 * k * k + 6 * k);  // CD: iters (2k^2 + 6k)
     }
+#ifdef CCD_PHASE_TIMERS
+    {
+        int wsw = (l >> 3) < NB ? sw : 0;  // the wave's sweep count: max over the band groups
+        for (int o = 32; o > 0; o >>= 1) {
+            const int t = __shfl_xor(wsw, o);
+            wsw = t > wsw ? t : wsw;
+        }
+        PH_COUNT(P, 28, wsw >= p.lasso_max_iter ? 1 : 0)
+        PH_COUNT(P, 29, wsw)
+        PH_COUNT(P, 30, wsw >= p.lasso_max_iter ? wsw : 0)
+    }
+#endif
     wsync();
     if (l < NB) {
         double dot = 0.0;
