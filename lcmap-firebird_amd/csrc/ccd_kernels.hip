@@ -369,26 +369,39 @@ __device__ __forceinline__ int compact_drop(Px &P, int a, F drop) {
     const int l = lane();
     int out = a;
     if (a < P.acc_b) P.acc_a = -1;  // rows of the accumulated Gram window may move
-    for (int base = a; base < P.m; base += W) {
-        const int j = base + l;
-        const bool in = j < P.m;
-        int32_t d = 0;
-        uint4 r = {0u, 0u, 0u, 0u};  // the 16-byte row as one vector (ci = high half of .w)
-        bool dr = false;
-        if (in) {
-            d = PCD(P)[j];
-            r = reinterpret_cast<const uint4 *>(PCR(P))[j];
-            dr = drop(j);
+    PH_COUNT(P, 31, P.m - a)
+    // four 64-row chunks per round: all their loads go out before the first store (a store lands
+    // at or below its row's old position, so it never overwrites a row still to be read)
+    constexpr int U = 4;
+    for (int base = a; base < P.m; base += U * W) {
+        int32_t d[U];
+        uint4 r[U];  // the 16-byte row as one vector (ci = high half of .w)
+        bool in[U], dr[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = base + u * W + l;
+            in[u] = j < P.m;
+            d[u] = 0;
+            r[u] = uint4{0u, 0u, 0u, 0u};
+            dr[u] = false;
+            if (in[u]) {
+                d[u] = PCD(P)[j];
+                r[u] = reinterpret_cast<const uint4 *>(PCR(P))[j];
+                dr[u] = drop(j);
+            }
         }
-        const unsigned long long keep = bal(in && !dr);
-        const unsigned ci = r.w >> 16;
-        if (in && dr) atomicAnd(&LDS().mask[ci >> 5], ~(1u << (ci & 31)));
-        if (in && !dr) {
-            const int pos = gidx(P, out + below(keep), P.n, __LINE__);
-            PCD(P)[pos] = d;
-            reinterpret_cast<uint4 *>(PCR(P))[pos] = r;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const unsigned long long keep = bal(in[u] && !dr[u]);
+            const unsigned ci = r[u].w >> 16;
+            if (in[u] && dr[u]) atomicAnd(&LDS().mask[ci >> 5], ~(1u << (ci & 31)));
+            if (in[u] && !dr[u]) {
+                const int pos = gidx(P, out + below(keep), P.n, __LINE__);
+                PCD(P)[pos] = d[u];
+                reinterpret_cast<uint4 *>(PCR(P))[pos] = r[u];
+            }
+            out += popc(keep);
         }
-        out += popc(keep);
     }
     P.m = out;
     psync();

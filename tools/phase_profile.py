@@ -30,7 +30,8 @@ for i, n in enumerate(counts):
 for i, n in enumerate(['spec early fits (CD)', 'closest: search', 'closest: run sum', 'closest: ties']):
     out[n] = dc[8 + 20 + i] / tot
 for i, n in enumerate(['batches ne<=16', 'batches ne<=32', 'batch valid lanes', 'batches without terminal step',
-                       'wave fits at max_iter', 'wave sweeps (single fits)', 'wave sweeps in max_iter fits']):
+                       'wave fits at max_iter', 'wave sweeps (single fits)', 'wave sweeps in max_iter fits',
+                       'compaction rows scanned']):
     out[n] = dc[8 + 24 + i]
 out['pixels'] = chips * 10000
 out['cycles_per_pixel'] = tot / out['pixels']
