@@ -2335,19 +2335,30 @@ __device__ __forceinline__ int px_setup(Px &P, int chip, int pix) {
     const int16_t *sp = A.spectra + (size_t)chip * NB * bstride + (size_t)pix * n;
     int c_clear = 0, c_water = 0, c_snow = 0, c_cloud = 0, c_fill = 0;
     bool bad = false;
-    for (int base = 0; base < n; base += W) {
-        const int i = base + l;
-        int cls = -2;
-        if (i < n) {
-            const unsigned q = qa[order[i]];
-            cls = p.qa_bitpacked ? qabitval(p, q) : (int)q;
+    // (four 64-observation chunks per round, their dependent order -> qa loads issued together)
+    constexpr int U = 4;
+    for (int base0 = 0; base0 < n; base0 += U * W) {
+        int o[U];
+        unsigned q[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = base0 + u * W + l;
+            o[u] = i < n ? order[i] : 0;
         }
-        c_clear += popc(bal(i < n && cls == p.qa_clear));
-        c_water += popc(bal(i < n && cls == p.qa_water));
-        c_snow += popc(bal(i < n && cls == p.qa_snow));
-        c_cloud += popc(bal(i < n && cls == p.qa_cloud));
-        c_fill += popc(bal(i < n && cls == p.qa_fill));
-        if (bal(i < n && cls < 0)) bad = true;
+#pragma unroll
+        for (int u = 0; u < U; ++u) q[u] = base0 + u * W + l < n ? (unsigned)qa[o[u]] : 0u;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = base0 + u * W + l;
+            int cls = -2;
+            if (i < n) cls = p.qa_bitpacked ? qabitval(p, q[u]) : (int)q[u];
+            c_clear += popc(bal(i < n && cls == p.qa_clear));
+            c_water += popc(bal(i < n && cls == p.qa_water));
+            c_snow += popc(bal(i < n && cls == p.qa_snow));
+            c_cloud += popc(bal(i < n && cls == p.qa_cloud));
+            c_fill += popc(bal(i < n && cls == p.qa_fill));
+            if (bal(i < n && cls < 0)) bad = true;
+        }
     }
     if (bad) return -1;
     const int total = n - c_fill;
@@ -2368,21 +2379,38 @@ __device__ __forceinline__ int px_setup(Px &P, int chip, int pix) {
     for (int i = l; i < A.mask_words; i += W) L->mask[i] = 0u;
     int m = 0;
     int carry = -1;  // date of the last kept observation (ordinals are >= 1)
-    for (int base = 0; base < n; base += W) {
+    constexpr int U2 = 2;  // two chunks per round: their gathers (order -> qa, 7 bands, date) together
+    for (int base0 = 0; base0 < n; base0 += U2 * W) {
+        int o2[U2], d2[U2];
+        unsigned q2[U2];
+        int16_t v2[U2][NB];
+#pragma unroll
+        for (int u = 0; u < U2; ++u) {
+            const int i = base0 + u * W + l;
+            o2[u] = i < n ? order[i] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U2; ++u) {
+            const int i = base0 + u * W + l;
+            const bool valid = i < n;
+            q2[u] = valid ? (unsigned)qa[o2[u]] : 0u;
+#pragma unroll
+            for (int b = 0; b < NB; ++b) v2[u][b] = valid ? sp[(size_t)b * bstride + o2[u]] : (int16_t)0;
+            d2[u] = valid ? (int)P.sd[i] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U2; ++u) {
+        const int base = base0 + u * W;
         const int i = base + l;
         const bool valid = i < n;
-        int cls = -2, d = 0;
+        int cls = -2;
+        const int d = d2[u];
         int16_t v[NB];
 #pragma unroll
-        for (int b = 0; b < NB; ++b) v[b] = 0;
+        for (int b = 0; b < NB; ++b) v[b] = v2[u][b];
         if (valid) {
-            const int o = order[i];
-            const unsigned q = qa[o];
-            cls = p.qa_bitpacked ? qabitval(p, q) : (int)q;
-#pragma unroll
-            for (int b = 0; b < NB; ++b) v[b] = sp[(size_t)b * bstride + o];
+            cls = p.qa_bitpacked ? qabitval(p, q2[u]) : (int)q2[u];
             if (conv) v[6] = (int16_t)((int)v[6] * 10 - 27315);
-            d = (int)P.sd[i];
         }
         const bool cwi = cls == p.qa_clear || cls == p.qa_water;
         const bool th = v[6] > p.thermal_min && v[6] < p.thermal_max;
@@ -2408,11 +2436,12 @@ __device__ __forceinline__ int px_setup(Px &P, int chip, int pix) {
             cw.ci = (uint16_t)i;
             PCR(P)[pos] = cw;
         }
-        if (l == 0) {
+        if (l == 0 && base < n) {
             L->mask[base >> 5] = (unsigned)k2;
             if (base + 32 < n) L->mask[(base >> 5) + 1] = (unsigned)(k2 >> 32);
         }
         m += popc(k2);
+        }
     }
     P.m = m;
     psync();
