@@ -888,7 +888,23 @@ __device__ __forceinline__ void variogram(Px &P) {
         return;
     }
     int lag = 0;
-    for (int k = 1; k < m; ++k) {
+    {
+        // lags 1..4 (where the lag is found nearly always) counted in one pass over the dates
+        int c4[4] = {0, 0, 0, 0};
+        for (int base = 0; base < m - 1; base += W) {
+            const int i = base + l;
+            const int d0 = i < m ? CDR(P, i) : 0;
+            int dk[4];
+#pragma unroll
+            for (int k = 1; k <= 4; ++k) dk[k - 1] = i + k < m ? CDR(P, i + k) : 0;
+#pragma unroll
+            for (int k = 1; k <= 4; ++k) c4[k - 1] += popc(bal(i + k < m && dk[k - 1] - d0 > 30));
+        }
+#pragma unroll
+        for (int k = 1; k <= 4; ++k)
+            if (!lag && k < m && 2 * c4[k - 1] >= m - k) lag = k;
+    }
+    for (int k = 5; !lag && k < m; ++k) {
         int cnt = 0;
         for (int base = 0; base < m - k; base += W) {
             const int i = base + l;
@@ -911,29 +927,41 @@ __device__ __forceinline__ void variogram(Px &P) {
     int small[NB];
 #pragma unroll
     for (int band = 0; band < NB; ++band) small[band] = 0;
-    for (int base = 0; base < m - kk; base += W) {
-        const int i = base + l;
-        bool ok = false;
-        uint4 r0 = {0u, 0u, 0u, 0u}, r1 = {0u, 0u, 0u, 0u};
-        if (i < m - kk) {
-            ok = all || (CDR(P, i + kk) - CDR(P, i)) > 30;
-            r0 = reinterpret_cast<const uint4 *>(PCR(P))[i];
-            r1 = reinterpret_cast<const uint4 *>(PCR(P))[i + kk];
-        }
-        const unsigned long long km = bal(ok);
-        const unsigned a0[4] = {r0.x, r0.y, r0.z, r0.w}, a1[4] = {r1.x, r1.y, r1.z, r1.w};
+    constexpr int U = 2;  // two chunks per round, loads before the stores
+    for (int base0 = 0; base0 < m - kk; base0 += U * W) {
+        bool okv[U];
+        uint4 r0v[U], r1v[U];
 #pragma unroll
-        for (int band = 0; band < NB; ++band) {
-            const int v0 = (int)(int16_t)(a0[band >> 1] >> ((band & 1) * 16));
-            const int v1 = (int)(int16_t)(a1[band >> 1] >> ((band & 1) * 16));
-            const int d = v1 - v0;
-            const int ad = d < 0 ? -d : d;
-            const bool lo = ok && ad < 256;
-            small[band] += popc(bal(lo));
-            if (ok) dv[band * stride + cnt + below(km)] = (uint16_t)ad;
-            if (lo) atomicAdd(&h16w[band * 128 + (ad >> 1)], 1u << ((ad & 1) * 16));
+        for (int u = 0; u < U; ++u) {
+            const int i = base0 + u * W + l;
+            okv[u] = false;
+            r0v[u] = uint4{0u, 0u, 0u, 0u};
+            r1v[u] = uint4{0u, 0u, 0u, 0u};
+            if (i < m - kk) {
+                okv[u] = all || (CDR(P, i + kk) - CDR(P, i)) > 30;
+                r0v[u] = reinterpret_cast<const uint4 *>(PCR(P))[i];
+                r1v[u] = reinterpret_cast<const uint4 *>(PCR(P))[i + kk];
+            }
         }
-        cnt += popc(km);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool ok = okv[u];
+            const uint4 r0 = r0v[u], r1 = r1v[u];
+            const unsigned long long km = bal(ok);
+            const unsigned a0[4] = {r0.x, r0.y, r0.z, r0.w}, a1[4] = {r1.x, r1.y, r1.z, r1.w};
+#pragma unroll
+            for (int band = 0; band < NB; ++band) {
+                const int v0 = (int)(int16_t)(a0[band >> 1] >> ((band & 1) * 16));
+                const int v1 = (int)(int16_t)(a1[band >> 1] >> ((band & 1) * 16));
+                const int d = v1 - v0;
+                const int ad = d < 0 ? -d : d;
+                const bool lo = ok && ad < 256;
+                small[band] += popc(bal(lo));
+                if (ok) dv[band * stride + cnt + below(km)] = (uint16_t)ad;
+                if (lo) atomicAdd(&h16w[band * 128 + (ad >> 1)], 1u << ((ad & 1) * 16));
+            }
+            cnt += popc(km);
+        }
     }
     gsync();
     for (int band = 0; band < NB; ++band) {
@@ -1652,9 +1680,18 @@ __device__ __forceinline__ void build_hist(const Px &P, int fa, int fb) {
     const int l = lane();
     for (int i = l; i < 732; i += W) L->hist2[i] = 0u;
     wsync();
-    for (int i = fa + l; i < fb; i += W) {
-        const int u = u1461(CDR(P, i));
-        atomicAdd(&L->hist2[u >> 1], 1u << ((u & 1) * 16));
+    // (four chunks per round: the date loads go out together)
+    for (int i0 = fa; i0 < fb; i0 += 4 * W) {
+        int dt[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) dt[u] = i0 + u * W + l < fb ? CDR(P, i0 + u * W + l) : 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (i0 + u * W + l < fb) {
+                const int b = u1461(dt[u]);
+                atomicAdd(&L->hist2[b >> 1], 1u << ((b & 1) * 16));
+            }
+        }
     }
     wsync();
 }
@@ -1686,29 +1723,52 @@ __device__ __forceinline__ void build_closest(const Px &P, int fa, int fb, int k
     double ssq[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) ssq[b] = 0.0;
-    for (int i = fa + l; i < fb; i += W) {
-        const uint4 q = reinterpret_cast<const uint4 *>(PCR(P))[gidx(P, i, P.m, __LINE__)];
-        const GLOBAL_AS double *bs = P.basis + (size_t)gidx(P, (int)(q.w >> 16), P.n, __LINE__) * CCD_BASIS_STRIDE;
-        double x[7];
+    // (two chunks per round: rows, design rows and dates of both loaded before the first store)
+    for (int i0 = fa; i0 < fb; i0 += 2 * W) {
+        uint4 qv[2];
+        int dt[2];
+        double xv[2][7];
 #pragma unroll
-        for (int c = 0; c < 7; ++c) x[c] = bs[c];
-        const int u = u1461(CDR(P, i));
-        const unsigned old = atomicAdd(&L->hist2[u >> 1], 1u << ((u & 1) * 16));
-        const int pos = gidx(P, (int)((old >> ((u & 1) * 16)) & 0xFFFFu), nf, __LINE__);
-        P.bk[pos] = (uint16_t)(i - fa);
-        const unsigned qw[4] = {q.x, q.y, q.z, q.w};
-        GLOBAL_AS double *o = P.fs + (size_t)pos * 8;
+        for (int u = 0; u < 2; ++u) {
+            const int i = i0 + u * W + l;
+            qv[u] = uint4{0u, 0u, 0u, 0u};
+            dt[u] = 0;
+            if (i < fb) {
+                qv[u] = reinterpret_cast<const uint4 *>(PCR(P))[gidx(P, i, P.m, __LINE__)];
+                dt[u] = CDR(P, i);
+            }
+        }
 #pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            const double *c = Lc->coef[b];
-            double pr = x[0] * c[0];
+        for (int u = 0; u < 2; ++u) {
+            const int i = i0 + u * W + l;
+            const GLOBAL_AS double *bs = P.basis + (size_t)gidx(P, i < fb ? (int)(qv[u].w >> 16) : 0, P.n, __LINE__) * CCD_BASIS_STRIDE;
 #pragma unroll
-            for (int jj = 1; jj < 7; ++jj) pr += x[jj] * c[jj];
-            pr += c[7];
-            const double y = (double)(int16_t)(qw[b >> 1] >> ((b & 1) * 16));
-            const double r = y - pr;
-            o[b] = r * r;
-            ssq[b] += r * r;
+            for (int c = 0; c < 7; ++c) xv[u][c] = bs[c];
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int i = i0 + u * W + l;
+            if (i >= fb) continue;
+            const uint4 q = qv[u];
+            const double *x = xv[u];
+            const int ub = u1461(dt[u]);
+            const unsigned old = atomicAdd(&L->hist2[ub >> 1], 1u << ((ub & 1) * 16));
+            const int pos = gidx(P, (int)((old >> ((ub & 1) * 16)) & 0xFFFFu), nf, __LINE__);
+            P.bk[pos] = (uint16_t)(i - fa);
+            const unsigned qw[4] = {q.x, q.y, q.z, q.w};
+            GLOBAL_AS double *o = P.fs + (size_t)pos * 8;
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                const double *c = Lc->coef[b];
+                double pr = x[0] * c[0];
+#pragma unroll
+                for (int jj = 1; jj < 7; ++jj) pr += x[jj] * c[jj];
+                pr += c[7];
+                const double y = (double)(int16_t)(qw[b >> 1] >> ((b & 1) * 16));
+                const double r = y - pr;
+                o[b] = r * r;
+                ssq[b] += r * r;
+            }
         }
     }
     const double den = (double)(nf - (ARGS().p.rmse_dof ? k : 0));
