@@ -1906,7 +1906,7 @@ __device__ __forceinline__ void comp_lane(Px &P, int nf, int dref, double (&cs)[
     PH_END(P, c1, 21)
     PH_BEGIN(c2)
     // (unrolled so several rows' loads are in flight; the sum stays in bucket order)
-#pragma unroll 4
+#pragma unroll 8
     for (int s = 0; s < less; ++s) {
         int pos = s0 + s;
         pos = pos >= nf ? pos - nf : pos;
