@@ -409,28 +409,9 @@ __device__ __forceinline__ int compact_drop(Px &P, int a, F drop) {
 }
 
 // ------------------------------------------------------------------ Lasso (models/lasso.py)
-// Stage rows j0 .. j0 + cnt - 1 of the period into the LDS tile as
+// gram_accumulate stages period rows into the LDS tile as
 // [t - t0, cos wt, sin wt, cos 2wt, sin 2wt, cos 3wt, sin 3wt, 1, y0 - s0 .. y6 - s6, 0]
 // (t0, s = the accumulated window's integer shifts: exact, and they keep the raw sums small).
-__device__ __forceinline__ void stage_rows(const Px &P, int j0, int cnt) {
-    Lds *L = &LDS();
-    const int l = lane();
-    if (l < cnt) {
-        const int j = j0 + l;
-        const CRow cw = CROW(P, j);
-        const GLOBAL_AS double *bs = P.basis + (size_t)cw.ci * CCD_BASIS_STRIDE;
-        double *r = L->row[l];
-        r[0] = bs[0] - (double)P.acc_t0;
-#pragma unroll
-        for (int c = 1; c < 7; ++c) r[c] = bs[c];
-        r[7] = 1.0;
-#pragma unroll
-        for (int b = 0; b < NB; ++b) r[8 + b] = (double)((int)cw.v[b] - L->y0[b]);
-        r[15] = 0.0;
-    }
-    wsync();
-}
-
 // Raw-sum entry e of the accumulated Gram: products of staged columns (ca, cb).  0..27 design
 // x design (upper triangle), 28..76 design x band, 77..83 band x band, 84..90 design sums,
 // 91..97 band sums; e >= 98 maps to the zero column.
@@ -479,14 +460,40 @@ __device__ __forceinline__ void gram_accumulate(Px &P, int a, int b) {
     gram_entry(l, ca0, cb0);
     gram_entry(l + W, ca1, cb1);
     double s0 = L->S[l], s1 = l + W < 98 ? L->S[l + W] : 0.0;
-    for (int t0 = from; t0 < b; t0 += TR) {
-        const int cnt = b - t0 < TR ? b - t0 : TR;
-        stage_rows(P, t0, cnt);
-        for (int r = 0; r < cnt; ++r) {
-            s0 += L->row[r][ca0] * L->row[r][cb0];
-            s1 += L->row[r][ca1] * L->row[r][cb1];
+    // 64 rows per round: every lane loads one row (period row + design row) up front, then the
+    // two 32-row halves are staged through the LDS tile in turn (one memory round trip per 64)
+    for (int t0 = from; t0 < b; t0 += 2 * TR) {
+        const int cnt = b - t0 < 2 * TR ? b - t0 : 2 * TR;
+        CRow cw{};
+        double x[7];
+#pragma unroll
+        for (int c = 0; c < 7; ++c) x[c] = 0.0;
+        if (l < cnt) {
+            cw = CROW(P, t0 + l);
+            const GLOBAL_AS double *bs = P.basis + (size_t)cw.ci * CCD_BASIS_STRIDE;
+#pragma unroll
+            for (int c = 0; c < 7; ++c) x[c] = bs[c];
         }
-        wsync();
+        for (int h = 0; h < 2; ++h) {
+            const int hc = cnt - h * TR < TR ? cnt - h * TR : TR;
+            if (hc <= 0) break;
+            if (l >= h * TR && l < h * TR + hc) {
+                double *r = L->row[l - h * TR];
+                r[0] = x[0] - (double)P.acc_t0;
+#pragma unroll
+                for (int c = 1; c < 7; ++c) r[c] = x[c];
+                r[7] = 1.0;
+#pragma unroll
+                for (int bb = 0; bb < NB; ++bb) r[8 + bb] = (double)((int)cw.v[bb] - L->y0[bb]);
+                r[15] = 0.0;
+            }
+            wsync();
+            for (int r = 0; r < hc; ++r) {
+                s0 += L->row[r][ca0] * L->row[r][cb0];
+                s1 += L->row[r][ca1] * L->row[r][cb1];
+            }
+            wsync();
+        }
     }
     L->S[l] = s0;
     if (l + W < 98) L->S[l + W] = s1;
