@@ -1927,8 +1927,16 @@ __device__ __forceinline__ void comp_lane(Px &P, int nf, int dref, double (&cs)[
     const int c1 = bcount(L, b1), c2 = K > 0 ? bcount(L, b2) : 0;
     const int st1 = bstart(L, b1), st2 = bstart(L, b2);
     const int T = c1 + c2;
+    // every entry at distance K is taken when there are no more of them than needed (no ranks)
+    const bool all_k = T <= need;
     for (int e = 0; e < T; ++e) {
         const int pe = e < c1 ? st1 + e : st2 + (e - c1);
+        if (all_k) {
+            const GLOBAL_AS double *f = P.fs + (size_t)gidx(P, pe, nf, __LINE__) * 8;
+#pragma unroll
+            for (int bd = 0; bd < NB; ++bd) cs[bd] += f[bd];
+            continue;
+        }
         const int ie = (int)P.bk[gidx(P, pe, P.n, __LINE__)];
         int rank = 0;
         for (int f2 = 0; f2 < T; ++f2) {
