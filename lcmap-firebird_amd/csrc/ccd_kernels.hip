@@ -613,14 +613,10 @@ __device__ __forceinline__ int cd_sweep(Lds *L, int pc_rt, double alpha, int max
         if (pc > 6) cd_coord<6>(k, live, alpha, gkk, rgkk, gcol[6], g, w);
         // every coordinate moves once per sweep: d_w_ii = |w_new - w_old| of the lane's own one
         const double d_w_max = gmax8(fabs(w - w0));
-        const double w_max = gmax8(act ? fabs(w) : 0.0);
-        // d_w_max / w_max < tol, with the division only where the quotient is near tol
-        const double tw = tol * w_max;
-        const bool near = !done && w_max != 0.0 && (w_max < 1e-280 || (d_w_max > 0.25 * tw && d_w_max < 4.0 * tw));
-        bool ratio_lt = d_w_max <= 0.25 * tw;
-        if (bal(near)) {
-            if (near) ratio_lt = d_w_max / w_max < tol;
-        }
+        const double w_max = gmax8(fabs(w));  // w stays 0 in lanes outside the model
+        // sklearn's d_w_max / w_max < tol, as one branch-free division (w_max = 0 is the check's
+        // own first clause)
+        const bool ratio_lt = d_w_max / w_max < tol;
         const bool check = !done && (w_max == 0.0 || ratio_lt || it == max_iter - 1);
         if (bal(check)) {
             const double xta = act ? g : 0.0;  // X^T R
@@ -2076,12 +2072,7 @@ __device__ __forceinline__ void spec_fits(Px &P, int a, int nw0, int V, SpecFit 
         double wmax = 0.0;
 #pragma unroll
         for (int i = 0; i < SPEC_PC; ++i) wmax = fmax(wmax, fabs(w[i]));  // w = 0 past pc
-        const double tw = tol * wmax;
-        const bool near = !done && wmax != 0.0 && (wmax < 1e-280 || (dmax > 0.25 * tw && dmax < 4.0 * tw));
-        bool ratio_lt = dmax <= 0.25 * tw;
-        if (bal(near)) {
-            if (near) ratio_lt = dmax / wmax < tol;
-        }
+        const bool ratio_lt = dmax / wmax < tol;  // (wmax = 0: the check's first clause)
         const bool check = !done && (wmax == 0.0 || ratio_lt || it == max_iter - 1);
         if (bal(check)) {
             double dual = 0.0, wq = 0.0, wxta = 0.0, l1 = 0.0;
