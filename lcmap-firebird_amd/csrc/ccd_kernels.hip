@@ -1893,12 +1893,12 @@ __device__ __forceinline__ void comp_lane(Px &P, int nf, int dref, double (&cs)[
     const int u = u1461(dref);
     int lo = 0, hi = 730;  // smallest K with cnt_within(K) >= 24
 #pragma unroll
-    for (int it = 0; it < 10; ++it) {
-        if (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (cnt_within(L, nf, u, mid) >= 24) hi = mid;
-            else lo = mid + 1;
-        }
+    for (int it = 0; it < 10; ++it) {  // branch-free: a finished lane re-reads its own bin
+        const int mid = (lo + hi) >> 1;
+        const bool ge = cnt_within(L, nf, u, mid) >= 24;
+        const bool act = lo < hi;
+        hi = act && ge ? mid : hi;
+        lo = act && !ge ? mid + 1 : lo;
     }
     const int K = lo;
     const int less = K > 0 ? cnt_within(L, nf, u, K - 1) : 0;
