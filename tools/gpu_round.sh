@@ -8,7 +8,7 @@ OUT="$R/gpurun_out"
 mkdir -p "$OUT"
 TAG=${1:-r01}
 STEPS=${STEPS:-all}
-run_tests() { timeout -k 10 900 python -m pytest tests -m gpu -x -q > "$OUT/${TAG}_pytest_gpu.log" 2>&1; }
+run_tests() { timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/${TAG}_pytest_gpu.log" 2>&1; }
 run_smoke() { timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/${TAG}_smoke.log" 2>&1; }
 run_bench() { timeout -k 10 600 python bench.py > "$OUT/${TAG}_bench.json" 2> "$OUT/${TAG}_bench.err"; }
 run_prof() {
