@@ -1668,9 +1668,14 @@ __device__ __forceinline__ void lookback(Px &P, int &wa, int &wb, int prev) {
 // The fit window and the model only change at a refit, so once per (fit window, model) the window
 // is counting-sorted by u into a bucket list (P.bk, fit-relative indices; L->hist2 keeps the bin
 // end positions) and every observation's squared residuals are stored in bucket order
-// (P.fs[pos * 8 + band]).  A lookforward step then needs no pass over the window: the bins closer
+// (P.fs[pos * FW + s], s-th detection band).  A lookforward step then needs no pass over the window: the bins closer
 // than K are one circular run of bucket positions, read with one coalesced load per band.
 __device__ __forceinline__ int u1461(int t) { return (4 * t) % 1461; }
+// The bucket-ordered squared residuals are kept for the detection bands only (the comparison rmse
+// enters change_magnitude and nothing else): row s of an entry is the s-th detection band, rows
+// are FSW(mask) doubles wide (5 for the default five bands, 7 otherwise; unused rows hold 0).
+__device__ __forceinline__ unsigned det_mask() { return ARGS().p.detection_bands & 0x7Fu; }
+__device__ __forceinline__ int fs_width(unsigned dm) { return __builtin_popcount(dm) <= 5 ? 5 : 7; }
 // L->hist2 holds two u16 per word: plain counts (closest_doy_scan) or, after build_closest, the
 // end position of each bin in the bucket list.
 __device__ __forceinline__ int h16(const Lds *L, int u) { return (int)((L->hist2[u >> 1] >> ((u & 1) * 16)) & 0xFFFFu); }
@@ -1723,6 +1728,8 @@ __device__ __forceinline__ void build_closest(const Px &P, int fa, int fb, int k
     // position (lane = observation: its row and design loads go out before the LDS atomic);
     // their sums are the models' rmse (lasso.fitted_model) over the same fit window.
     const Lds *Lc = L;
+    const unsigned dm = det_mask();
+    const int nd = __builtin_popcount(dm), fw = fs_width(dm);
     double ssq[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) ssq[b] = 0.0;
@@ -1759,7 +1766,7 @@ __device__ __forceinline__ void build_closest(const Px &P, int fa, int fb, int k
             const int pos = gidx(P, (int)((old >> ((ub & 1) * 16)) & 0xFFFFu), nf, __LINE__);
             P.bk[pos] = (uint16_t)(i - fa);
             const unsigned qw[4] = {q.x, q.y, q.z, q.w};
-            GLOBAL_AS double *o = P.fs + (size_t)pos * 8;
+            GLOBAL_AS double *o = P.fs + (size_t)pos * fw;
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
                 const double *c = Lc->coef[b];
@@ -1769,9 +1776,10 @@ __device__ __forceinline__ void build_closest(const Px &P, int fa, int fb, int k
                 pr += c[7];
                 const double y = (double)(int16_t)(qw[b >> 1] >> ((b & 1) * 16));
                 const double r = y - pr;
-                o[b] = r * r;
+                if ((dm >> b) & 1u) o[__builtin_popcount(dm & ((1u << b) - 1u))] = r * r;
                 ssq[b] += r * r;
             }
+            for (int t = nd; t < fw; ++t) o[t] = 0.0;
         }
     }
     const double den = (double)(nf - (ARGS().p.rmse_dof ? k : 0));
@@ -1887,6 +1895,7 @@ __device__ __forceinline__ int cnt_within(const Lds *L, int nf, int u, int d) {
 // from the bucket list and bucket-ordered squared residuals build_closest left (nf > 24).
 // Entries at distance < K form one circular run of bucket positions; at distance exactly K the
 // lowest fit-relative indices win (stable argsort).
+template <int FW>
 __device__ __forceinline__ void comp_lane(Px &P, int nf, int dref, double (&cs)[NB]) {
     const Lds *L = &LDS();
     PH_BEGIN(c1)
@@ -1913,9 +1922,9 @@ __device__ __forceinline__ void comp_lane(Px &P, int nf, int dref, double (&cs)[
     for (int s = 0; s < less; ++s) {
         int pos = s0 + s;
         pos = pos >= nf ? pos - nf : pos;
-        const GLOBAL_AS double *f = P.fs + (size_t)gidx(P, pos, nf, __LINE__) * 8;
+        const GLOBAL_AS double *f = P.fs + (size_t)gidx(P, pos, nf, __LINE__) * FW;
 #pragma unroll
-        for (int bd = 0; bd < NB; ++bd) cs[bd] += f[bd];
+        for (int bd = 0; bd < FW; ++bd) cs[bd] += f[bd];
     }
     PH_END(P, c2, 22)
     PH_BEGIN(c3)
@@ -1928,9 +1937,9 @@ __device__ __forceinline__ void comp_lane(Px &P, int nf, int dref, double (&cs)[
     for (int e = 0; e < T; ++e) {
         const int pe = e < c1 ? st1 + e : st2 + (e - c1);
         if (all_k) {
-            const GLOBAL_AS double *f = P.fs + (size_t)gidx(P, pe, nf, __LINE__) * 8;
+            const GLOBAL_AS double *f = P.fs + (size_t)gidx(P, pe, nf, __LINE__) * FW;
 #pragma unroll
-            for (int bd = 0; bd < NB; ++bd) cs[bd] += f[bd];
+            for (int bd = 0; bd < FW; ++bd) cs[bd] += f[bd];
             continue;
         }
         const int ie = (int)P.bk[gidx(P, pe, P.n, __LINE__)];
@@ -1940,13 +1949,13 @@ __device__ __forceinline__ void comp_lane(Px &P, int nf, int dref, double (&cs)[
             rank += ((int)P.bk[gidx(P, pf, P.n, __LINE__)] < ie) ? 1 : 0;
         }
         if (rank < need) {
-            const GLOBAL_AS double *f = P.fs + (size_t)gidx(P, pe, nf, __LINE__) * 8;
+            const GLOBAL_AS double *f = P.fs + (size_t)gidx(P, pe, nf, __LINE__) * FW;
 #pragma unroll
-            for (int bd = 0; bd < NB; ++bd) cs[bd] += f[bd];
+            for (int bd = 0; bd < FW; ++bd) cs[bd] += f[bd];
         }
     }
 #pragma unroll
-    for (int bd = 0; bd < NB; ++bd) cs[bd] = sqrt(cs[bd]) / 4.0;
+    for (int bd = 0; bd < FW; ++bd) cs[bd] = sqrt(cs[bd]) / 4.0;
     PH_END(P, c3, 23)
 }
 
@@ -2266,33 +2275,48 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
         bool allc = false, outj = false;
         if (valid) {
             dj = CDR(P, x0 + l);
+            // comparison rmse per detection band: cs[s] for the s-th detection band bs[s]
+            const unsigned dm = det_mask();
+            const int nd = __builtin_popcount(dm);
+            int bs[NB];
+            unsigned rest = dm;
+#pragma unroll
+            for (int t = 0; t < NB; ++t) {
+                bs[t] = rest ? __builtin_ctz(rest) : 0;
+                rest &= rest - 1u;
+            }
             double cs[NB];
+#pragma unroll
+            for (int t = 0; t < NB; ++t) cs[t] = 0.0;
             PH_BEGIN(cmp)
             if (nf > 24) {
-                comp_lane(P, nf, CDR(P, x0 + l + k - 1), cs);
+                const int dref = CDR(P, x0 + l + k - 1);
+                if (fs_width(dm) == 5) comp_lane<5>(P, nf, dref, cs);
+                else comp_lane<7>(P, nf, dref, cs);
             } else {
 #pragma unroll
-                for (int bd = 0; bd < NB; ++bd) cs[bd] = L->comp[bd];
+                for (int t = 0; t < NB; ++t) cs[t] = L->comp[bs[t]];
             }
             PH_END(P, cmp, 14)
             PH_BEGIN(mg)
             const double *R = PRES(L) + l;
-            // change_magnitude: (r / max(vario, comp))^2 summed over the detection bands, with the
-            // division as a multiply by the band's reciprocal (one division per band and step)
+            // change_magnitude: (r / max(vario, comp))^2 summed over the detection bands (in band
+            // order), with the division as a multiply by the band's reciprocal (one division per
+            // band and step)
             double irm[NB];
 #pragma unroll
-            for (int bd = 0; bd < NB; ++bd) {
-                const double vr = L->vario[bd], cr = cs[bd];
+            for (int t = 0; t < NB; ++t) {
+                const double vr = L->vario[bs[t]], cr = cs[t];
                 const double rm = (vr != vr || cr != cr) ? __builtin_nan("") : (vr > cr ? vr : cr);
-                irm[bd] = ((p.detection_bands >> bd) & 1u) ? 1.0 / rm : 0.0;
+                irm[t] = t < nd ? 1.0 / rm : 0.0;
             }
             allc = true;
             for (int jj = 0; jj < k; ++jj) {
                 double mg = 0.0;
 #pragma unroll
-                for (int bd = 0; bd < NB; ++bd) {
-                    if ((p.detection_bands >> bd) & 1u) {
-                        const double v = R[bd * W + jj] * irm[bd];
+                for (int t = 0; t < NB; ++t) {
+                    if (t < nd) {
+                        const double v = R[bs[t] * W + jj] * irm[t];
                         mg += v * v;
                     }
                 }
@@ -2616,6 +2640,7 @@ __device__ __forceinline__ void detect_body() {
 __global__ __launch_bounds__(64) __attribute__((flatten)) void ccd_detect() { detect_body(); }
 __global__ __launch_bounds__(64, 2) __attribute__((flatten)) void ccd_detect_w2() { detect_body(); }
 __global__ __launch_bounds__(64, 3) __attribute__((flatten)) void ccd_detect_w3() { detect_body(); }
+__global__ __launch_bounds__(64, 4) __attribute__((flatten)) void ccd_detect_w4() { detect_body(); }
 
 // ------------------------------------------------------------------ per-chip preparation
 // One 256-thread block per chip: stable rank of each date (ties by input position), sorted
@@ -2707,6 +2732,7 @@ static const void *detect_fn(int variant) {
     switch (variant) {
     case 1: return reinterpret_cast<const void *>(&ccd_detect);
     case 2: return reinterpret_cast<const void *>(&ccd_detect_w2);
+    case 4: return reinterpret_cast<const void *>(&ccd_detect_w4);
     default: return reinterpret_cast<const void *>(&ccd_detect_w3);
     }
 }
@@ -2726,6 +2752,7 @@ extern "C" int ccdk_detect(int32_t grid, int variant, int32_t n_obs, void *strea
     switch (variant) {
     case 1: hipLaunchKernelGGL(ccd_detect, dim3(grid), dim3(64), lds, (hipStream_t)stream); break;
     case 2: hipLaunchKernelGGL(ccd_detect_w2, dim3(grid), dim3(64), lds, (hipStream_t)stream); break;
+    case 4: hipLaunchKernelGGL(ccd_detect_w4, dim3(grid), dim3(64), lds, (hipStream_t)stream); break;
     default: hipLaunchKernelGGL(ccd_detect_w3, dim3(grid), dim3(64), lds, (hipStream_t)stream); break;
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -250,7 +250,7 @@ int ccdgpu_init(int device, ccdgpu_ctx **out) {
     c->slots_per_cu = 16;
     c->variant = ccdk_period_in_lds() ? 1 : 3;
     if (const char *v = std::getenv("CCDGPU_KERNEL")) {
-        if (v[0] == 'w' && v[1] >= '1' && v[1] <= '3' && v[2] == 0) c->variant = v[1] - '0';
+        if (v[0] == 'w' && v[1] >= '1' && v[1] <= '4' && v[2] == 0) c->variant = v[1] - '0';
     }
     if (const char *v = std::getenv("CCDGPU_SLOTS_PER_CU")) c->slots_per_cu = std::max(1, std::atoi(v));
     *out = c;

@@ -52,6 +52,7 @@ def test_chip_vs_oracle(ctx, which, chip, n_pix):
     {'PEEK_SIZE': 8, 'ADAPTIVE_PEEK': False},
     {'T_CONST': 4.89, 'CHANGE_PROBABILITY': 0.95},
     {'DETECTION_BANDS': [1, 3, 4], 'TMASK_BANDS': [2, 4]},
+    {'DETECTION_BANDS': [0, 1, 2, 3, 4, 5, 6]},
     {'KELVIN_TO_CELSIUS': False, 'THERMAL_MIN': 1800, 'THERMAL_MAX': 3400},
     {'COEFFICIENT_MAX': 6, 'LASSO_MAX_ITER': 50},
 ])
