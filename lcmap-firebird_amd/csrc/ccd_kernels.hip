@@ -1917,14 +1917,32 @@ __device__ __forceinline__ void comp_lane(Px &P, int nf, int dref, double (&cs)[
     const int s0 = K > 0 ? bstart(L, (u - K + 1 + 1461) % 1461) : 0;
     PH_END(P, c1, 21)
     PH_BEGIN(c2)
-    // (unrolled so several rows' loads are in flight; the sum stays in bucket order)
-#pragma unroll 8
-    for (int s = 0; s < less; ++s) {
-        int pos = s0 + s;
-        pos = pos >= nf ? pos - nf : pos;
-        const GLOBAL_AS double *f = P.fs + (size_t)gidx(P, pos, nf, __LINE__) * FW;
+    // Rounds of RS rows: every row's loads are issued before the first add (the rows of a round
+    // beyond `less` re-read row 0 and are added with weight 0: fma(f, 1, c) is the plain add, so
+    // the sum stays exactly the bucket-order sum).
+#ifndef CCD_RS
+#define CCD_RS 4
+#endif
+    constexpr int RS = CCD_RS;
+    const int s0w = s0 >= nf ? s0 - nf : s0;  // bucket position of row 0 (s0 may equal nf)
+    for (int s = 0; s < less; s += RS) {
+        double f[RS][FW];
+        double wt[RS];
 #pragma unroll
-        for (int bd = 0; bd < FW; ++bd) cs[bd] += f[bd];
+        for (int u = 0; u < RS; ++u) {
+            int pos = s0 + s + u;
+            pos = pos >= nf ? pos - nf : pos;
+            const bool ok = s + u < less;
+            wt[u] = ok ? 1.0 : 0.0;
+            const GLOBAL_AS double *fp = P.fs + (size_t)gidx(P, ok ? pos : s0w, nf, __LINE__) * FW;
+#pragma unroll
+            for (int bd = 0; bd < FW; ++bd) f[u][bd] = fp[bd];
+        }
+#pragma unroll
+        for (int u = 0; u < RS; ++u) {
+#pragma unroll
+            for (int bd = 0; bd < FW; ++bd) cs[bd] = fma(f[u][bd], wt[u], cs[bd]);
+        }
     }
     PH_END(P, c2, 22)
     PH_BEGIN(c3)
