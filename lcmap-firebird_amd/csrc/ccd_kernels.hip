@@ -477,20 +477,35 @@ __device__ __forceinline__ void gram_accumulate(Px &P, int a, int b) {
         for (int h = 0; h < 2; ++h) {
             const int hc = cnt - h * TR < TR ? cnt - h * TR : TR;
             if (hc <= 0) break;
-            if (l >= h * TR && l < h * TR + hc) {
+            const int hc4 = (hc + 3) & ~3;  // rows hc .. hc4 - 1 are staged as zeros (add nothing)
+            if (l >= h * TR && l < h * TR + hc4) {
+                const bool rv = l < h * TR + hc;
                 double *r = L->row[l - h * TR];
-                r[0] = x[0] - (double)P.acc_t0;
+                r[0] = rv ? x[0] - (double)P.acc_t0 : 0.0;
 #pragma unroll
-                for (int c = 1; c < 7; ++c) r[c] = x[c];
-                r[7] = 1.0;
+                for (int c = 1; c < 7; ++c) r[c] = rv ? x[c] : 0.0;
+                r[7] = rv ? 1.0 : 0.0;
 #pragma unroll
-                for (int bb = 0; bb < NB; ++bb) r[8 + bb] = (double)((int)cw.v[bb] - L->y0[bb]);
+                for (int bb = 0; bb < NB; ++bb) r[8 + bb] = rv ? (double)((int)cw.v[bb] - L->y0[bb]) : 0.0;
                 r[15] = 0.0;
             }
             wsync();
-            for (int r = 0; r < hc; ++r) {
-                s0 += L->row[r][ca0] * L->row[r][cb0];
-                s1 += L->row[r][ca1] * L->row[r][cb1];
+            // four rows per round, all sixteen LDS reads issued before the first FMA (the sums
+            // stay sequential over the rows)
+            for (int r = 0; r < hc4; r += 4) {
+                double a0[4], b0[4], a1[4], b1[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    a0[u] = L->row[r + u][ca0];
+                    b0[u] = L->row[r + u][cb0];
+                    a1[u] = L->row[r + u][ca1];
+                    b1[u] = L->row[r + u][cb1];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    s0 += a0[u] * b0[u];
+                    s1 += a1[u] * b1[u];
+                }
             }
             wsync();
         }
@@ -1029,6 +1044,22 @@ __device__ __forceinline__ void tm_row(const Px &P, int j, int i, int ncol, cons
     }
 }
 
+// acc += w x_ea x_eb over staged rows 0 .. cnt4 - 1 (cnt4 a multiple of 4), sequential over the
+// rows, four rows per round with all their LDS reads issued before the first multiply
+__device__ __forceinline__ void tm_rows_acc(const Lds *L, int cnt4, int ea, int eb, double &acc) {
+    for (int r = 0; r < cnt4; r += 4) {
+        double wv[4], xa[4], xb[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            wv[u] = L->row[r + u][5];
+            xa[u] = L->row[r + u][ea];
+            xb[u] = L->row[r + u][eb];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += wv[u] * xa[u] * xb[u];
+    }
+}
+
 // normal equations sum w x x^T and sum w x y over the window into L->G[0..4][0..4] and
 // L->Q[0..4][0]: rows [x0..x4, w, y] staged in LDS 64 at a time, lane = matrix entry,
 // sequential over rows (same scheme as the Lasso Gram in fit_models).
@@ -1049,6 +1080,7 @@ __device__ __forceinline__ void tm_normal(const Px &P, int a, int nw, int ncol, 
     double acc = 0.0;
     for (int t0 = 0; t0 < nw; t0 += TR) {
         const int cnt = nw - t0 < TR ? nw - t0 : TR;
+        const int cnt4 = (cnt + 3) & ~3;  // rows cnt .. cnt4 - 1 staged as zeros (add nothing)
         if (l < cnt) {
             const int i = t0 + l;
             double x[5];
@@ -1058,10 +1090,13 @@ __device__ __forceinline__ void tm_normal(const Px &P, int a, int nw, int ncol, 
             for (int r = 0; r < 5; ++r) row[r] = x[r];
             row[5] = wv ? wv[i] : 1.0;
             row[6] = band >= 0 ? cvalf(P, band, a + i) : 0.0;
+        } else if (l < cnt4) {
+            double *row = L->row[l];
+#pragma unroll
+            for (int r = 0; r < 7; ++r) row[r] = 0.0;
         }
         wsync();
-        if (ea >= 0)
-            for (int r = 0; r < cnt; ++r) acc += L->row[r][5] * L->row[r][ea] * L->row[r][eb];
+        if (ea >= 0) tm_rows_acc(L, cnt4, ea, eb, acc);
         wsync();
     }
     if (l < 15) {
@@ -1175,16 +1210,17 @@ __device__ __forceinline__ void tm_normal_reg(const double (&x)[5], double wv, d
     double acc = 0.0;
     for (int t0 = 0; t0 < nw; t0 += TR) {
         const int cnt = nw - t0 < TR ? nw - t0 : TR;
-        if (l >= t0 && l < t0 + cnt) {
+        const int cnt4 = (cnt + 3) & ~3;  // rows cnt .. cnt4 - 1 staged as zeros (add nothing)
+        if (l >= t0 && l < t0 + cnt4) {
+            const bool rv = l < t0 + cnt;
             double *row = L->row[l - t0];
 #pragma unroll
-            for (int r = 0; r < 5; ++r) row[r] = x[r];
-            row[5] = wv;
-            row[6] = yv;
+            for (int r = 0; r < 5; ++r) row[r] = rv ? x[r] : 0.0;
+            row[5] = rv ? wv : 0.0;
+            row[6] = rv ? yv : 0.0;
         }
         wsync();
-        if (ea >= 0)
-            for (int r = 0; r < cnt; ++r) acc += L->row[r][5] * L->row[r][ea] * L->row[r][eb];
+        if (ea >= 0) tm_rows_acc(L, cnt4, ea, eb, acc);
         wsync();
     }
     if (l < 15) {
@@ -1712,15 +1748,21 @@ __device__ __forceinline__ void build_closest(const Px &P, int fa, int fb, int k
     const int nf = fb - fa;
     build_hist(P, fa, fb);
     // exclusive prefix over the 1461 bins: lane l owns words [12 l, 12 l + 12) (24 bins)
+    // (the lane's 12 words read at once: 732 = 61 lanes x 12)
+    unsigned hv[12];
+    const bool hl = l < 61;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) hv[i] = hl ? L->hist2[12 * l + i] : 0u;
     int tot = 0;
-    for (int w = 12 * l; w < 12 * l + 12 && w < 732; ++w) tot += (int)(L->hist2[w] & 0xFFFFu) + (int)(L->hist2[w] >> 16);
+#pragma unroll
+    for (int i = 0; i < 12; ++i) tot += (int)(hv[i] & 0xFFFFu) + (int)(hv[i] >> 16);
     int run = wscan_incl(tot) - tot;
-    for (int w = 12 * l; w < 12 * l + 12 && w < 732; ++w) {
-        const unsigned v = L->hist2[w];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
         const int s0 = run;
-        const int s1 = run + (int)(v & 0xFFFFu);
-        run = s1 + (int)(v >> 16);
-        L->hist2[w] = (unsigned)s0 | ((unsigned)s1 << 16);  // bin start positions
+        const int s1 = run + (int)(hv[i] & 0xFFFFu);
+        run = s1 + (int)(hv[i] >> 16);
+        if (hl) L->hist2[12 * l + i] = (unsigned)s0 | ((unsigned)s1 << 16);  // bin start positions
     }
     wsync();
     // fill: each add advances the bin's cursor, so afterwards every bin holds its end position.
@@ -2329,17 +2371,28 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
                 irm[t] = t < nd ? 1.0 / rm : 0.0;
             }
             allc = true;
-            for (int jj = 0; jj < k; ++jj) {
-                double mg = 0.0;
+            // four peek observations per round, their ring reads issued before the first multiply
+            // (rounds past k read other ring entries; their magnitudes are not used)
+            for (int j0 = 0; j0 < k; j0 += 4) {
+                double rv[4][NB];
 #pragma unroll
-                for (int t = 0; t < NB; ++t) {
-                    if (t < nd) {
-                        const double v = R[bs[t] * W + jj] * irm[t];
-                        mg += v * v;
-                    }
+                for (int u = 0; u < 4; ++u) {
+#pragma unroll
+                    for (int t = 0; t < NB; ++t) rv[u][t] = t < nd ? R[bs[t] * W + j0 + u] : 0.0;
                 }
-                allc = allc && (mg > P.chg);
-                if (jj == 0) outj = mg > p.outlier_threshold;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    double mg = 0.0;
+#pragma unroll
+                    for (int t = 0; t < NB; ++t) {
+                        if (t < nd) {
+                            const double v = rv[u][t] * irm[t];
+                            mg += v * v;
+                        }
+                    }
+                    allc = allc && (j0 + u >= k || mg > P.chg);
+                    if (j0 + u == 0) outj = mg > p.outlier_threshold;
+                }
             }
             PH_END(P, mg, 15)
         }
