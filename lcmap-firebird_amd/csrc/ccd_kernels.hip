@@ -1775,20 +1775,29 @@ __device__ __forceinline__ void build_closest(const Px &P, int fa, int fb, int k
     double ssq[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) ssq[b] = 0.0;
-    // (two chunks per round: rows, design rows and dates of both loaded before the first store)
+    // Two chunks per round, software-pipelined: the next round's rows and dates load while this
+    // round's design rows load and its entries are filled, so a round exposes one memory round
+    // trip (the design rows, which need the row's sorted index) instead of two.
+    uint4 qn[2];
+    int dn[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int i = fa + u * W + l;
+        qn[u] = uint4{0u, 0u, 0u, 0u};
+        dn[u] = 0;
+        if (i < fb) {
+            qn[u] = reinterpret_cast<const uint4 *>(PCR(P))[gidx(P, i, P.m, __LINE__)];
+            dn[u] = CDR(P, i);
+        }
+    }
     for (int i0 = fa; i0 < fb; i0 += 2 * W) {
         uint4 qv[2];
         int dt[2];
         double xv[2][7];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            const int i = i0 + u * W + l;
-            qv[u] = uint4{0u, 0u, 0u, 0u};
-            dt[u] = 0;
-            if (i < fb) {
-                qv[u] = reinterpret_cast<const uint4 *>(PCR(P))[gidx(P, i, P.m, __LINE__)];
-                dt[u] = CDR(P, i);
-            }
+            qv[u] = qn[u];
+            dt[u] = dn[u];
         }
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -1796,6 +1805,16 @@ __device__ __forceinline__ void build_closest(const Px &P, int fa, int fb, int k
             const GLOBAL_AS double *bs = P.basis + (size_t)gidx(P, i < fb ? (int)(qv[u].w >> 16) : 0, P.n, __LINE__) * CCD_BASIS_STRIDE;
 #pragma unroll
             for (int c = 0; c < 7; ++c) xv[u][c] = bs[c];
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int i = i0 + (2 + u) * W + l;
+            qn[u] = uint4{0u, 0u, 0u, 0u};
+            dn[u] = 0;
+            if (i < fb) {
+                qn[u] = reinterpret_cast<const uint4 *>(PCR(P))[gidx(P, i, P.m, __LINE__)];
+                dn[u] = CDR(P, i);
+            }
         }
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
