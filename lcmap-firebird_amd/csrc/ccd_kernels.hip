@@ -2013,7 +2013,44 @@ __device__ __forceinline__ void comp_lane(Px &P, int nf, int dref, double (&cs)[
     const int T = c1 + c2;
     // every entry at distance K is taken when there are no more of them than needed (no ranks)
     const bool all_k = T <= need;
-    for (int e = 0; e < T; ++e) {
+    constexpr int TU = 8;
+    if (T <= TU) {
+        // up to 8 entries: their fit indices loaded at once and ranked in registers, then their
+        // squared residuals added in entry order (weight 0 for the entries not taken)
+        int iv[TU], pe[TU];
+#pragma unroll
+        for (int e = 0; e < TU; ++e) {
+            pe[e] = e < T ? (e < c1 ? st1 + e : st2 + (e - c1)) : 0;
+            pe[e] = gidx(P, pe[e], nf, __LINE__);
+        }
+#pragma unroll
+        for (int e = 0; e < TU; ++e) iv[e] = (!all_k && e < T) ? (int)P.bk[pe[e]] : 0x7FFFFFFF;
+        double ws[TU];
+#pragma unroll
+        for (int e = 0; e < TU; ++e) {
+            int rank = 0;
+#pragma unroll
+            for (int f = 0; f < TU; ++f) rank += iv[f] < iv[e] ? 1 : 0;
+            ws[e] = (e < T && (all_k || rank < need)) ? 1.0 : 0.0;
+        }
+#pragma unroll
+        for (int e0 = 0; e0 < TU; e0 += 4) {
+            if (e0 >= T) break;
+            double f[4][FW];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const GLOBAL_AS double *fp = P.fs + (size_t)pe[e0 + u] * FW;
+#pragma unroll
+                for (int bd = 0; bd < FW; ++bd) f[u][bd] = fp[bd];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+#pragma unroll
+                for (int bd = 0; bd < FW; ++bd) cs[bd] = fma(f[u][bd], ws[e0 + u], cs[bd]);
+            }
+        }
+    }
+    for (int e = 0; e < (T <= TU ? 0 : T); ++e) {
         const int pe = e < c1 ? st1 + e : st2 + (e - c1);
         if (all_k) {
             const GLOBAL_AS double *f = P.fs + (size_t)gidx(P, pe, nf, __LINE__) * FW;
@@ -2515,18 +2552,24 @@ __device__ __forceinline__ int px_setup(Px &P, int chip, int pix) {
     const int16_t *sp = A.spectra + (size_t)chip * NB * bstride + (size_t)pix * n;
     int c_clear = 0, c_water = 0, c_snow = 0, c_cloud = 0, c_fill = 0;
     bool bad = false;
-    // (four 64-observation chunks per round, their dependent order -> qa loads issued together)
+    // (four 64-observation chunks per round, their dependent order -> qa loads issued together;
+    // the next round's order loads go out with this round's qa loads)
     constexpr int U = 4;
+    int on[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) on[u] = u * W + l < n ? order[u * W + l] : 0;
     for (int base0 = 0; base0 < n; base0 += U * W) {
         int o[U];
         unsigned q[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int i = base0 + u * W + l;
-            o[u] = i < n ? order[i] : 0;
-        }
+        for (int u = 0; u < U; ++u) o[u] = on[u];
 #pragma unroll
         for (int u = 0; u < U; ++u) q[u] = base0 + u * W + l < n ? (unsigned)qa[o[u]] : 0u;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = base0 + (U + u) * W + l;
+            on[u] = i < n ? order[i] : 0;
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int i = base0 + u * W + l;
@@ -2559,16 +2602,17 @@ __device__ __forceinline__ int px_setup(Px &P, int chip, int pix) {
     for (int i = l; i < A.mask_words; i += W) L->mask[i] = 0u;
     int m = 0;
     int carry = -1;  // date of the last kept observation (ordinals are >= 1)
-    constexpr int U2 = 2;  // two chunks per round: their gathers (order -> qa, 7 bands, date) together
+    constexpr int U2 = 2;  // two chunks per round: their gathers (order -> qa, 7 bands, date) together,
+                           // the next round's order loads with them
+    int on2[U2];
+#pragma unroll
+    for (int u = 0; u < U2; ++u) on2[u] = u * W + l < n ? order[u * W + l] : 0;
     for (int base0 = 0; base0 < n; base0 += U2 * W) {
         int o2[U2], d2[U2];
         unsigned q2[U2];
         int16_t v2[U2][NB];
 #pragma unroll
-        for (int u = 0; u < U2; ++u) {
-            const int i = base0 + u * W + l;
-            o2[u] = i < n ? order[i] : 0;
-        }
+        for (int u = 0; u < U2; ++u) o2[u] = on2[u];
 #pragma unroll
         for (int u = 0; u < U2; ++u) {
             const int i = base0 + u * W + l;
@@ -2577,6 +2621,11 @@ __device__ __forceinline__ int px_setup(Px &P, int chip, int pix) {
 #pragma unroll
             for (int b = 0; b < NB; ++b) v2[u][b] = valid ? sp[(size_t)b * bstride + o2[u]] : (int16_t)0;
             d2[u] = valid ? (int)P.sd[i] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U2; ++u) {
+            const int i = base0 + (U2 + u) * W + l;
+            on2[u] = i < n ? order[i] : 0;
         }
 #pragma unroll
         for (int u = 0; u < U2; ++u) {
