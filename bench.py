@@ -44,6 +44,8 @@ def parse():
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--chips', type=int, default=64, help='chips per GPU per step')
     ap.add_argument('--config', type=int, default=3, help='synthetic config (2, 3, 4 or 5)')
+    ap.add_argument('--contexts', type=int, default=2,
+                    help='contexts per GPU running steps concurrently (each stages the same chips)')
     ap.add_argument('--cpu-seconds', type=float, default=12.0, help='target CPU-baseline sample time')
     ap.add_argument('--cpu-threads', type=int, default=16)
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -92,27 +94,44 @@ def main():
         assert np.array_equal(d, dates)
         D[j], S[j], Q[j] = d, s, q
 
-    ctx = ccdgpu.Context(local)
-    ctx.stage(D, S, Q)
+    ctxs = [ccdgpu.Context(local) for _ in range(max(1, args.contexts))]
+    for c in ctxs:
+        c.stage(D, S, Q)
+    ctx = ctxs[0]
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
     for _ in range(args.warmup):
-        ctx.run()
+        for c in ctxs:
+            c.run()
     barrier()
     ctx.synchronize()
     t0 = time.perf_counter()
-    det_ms, prep_ms, flops, segs = [], [], 0, 0
-    for _ in range(args.steps):
-        ctx.run()
-        st = ctx.stats()
-        det_ms.append(st['detect_ms'])
-        prep_ms.append(st['prep_ms'])
-        flops = st['flops']
-        segs = st['segments']
-        alg_bytes = st['bytes']
+    det_ms, prep_ms = [], []
+    last = {}
+
+    def steps_on(c, k):
+        # k steps on context c (ctypes releases the GIL: contexts run concurrently)
+        for _ in range(k):
+            c.run()
+            st = c.stats()
+            det_ms.append(st['detect_ms'])
+            prep_ms.append(st['prep_ms'])
+            last.update(st)
+
+    if len(ctxs) == 1:
+        steps_on(ctx, args.steps)
+    else:
+        import threading
+        share = [args.steps // len(ctxs) + (1 if i < args.steps % len(ctxs) else 0) for i in range(len(ctxs))]
+        th = [threading.Thread(target=steps_on, args=(c, k)) for c, k in zip(ctxs, share)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+    flops, segs, alg_bytes = last['flops'], last['segments'], last['bytes']
     ctx.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -125,7 +144,10 @@ def main():
     pixels_total = world * len(ids) * PIXELS_PER_CHIP * args.steps
     value = pixels_total / elapsed
     det_avg = float(np.mean(det_ms))
-    achieved_tf = flops / (det_avg * 1e-3) / 1e12
+    # per-launch time behind the roofline: the HIP-event launch duration; with concurrent contexts
+    # the launches overlap, so the wall time per launch (elapsed / steps) is the effective one
+    launch_ms = det_avg if len(ctxs) == 1 else elapsed * 1e3 / args.steps
+    achieved_tf = flops / (launch_ms * 1e-3) / 1e12
     traffic = None
     pmc_path = os.path.join(ROOT, 'profiles', 'pmc_detect.json')
     if os.path.exists(pmc_path):
@@ -152,7 +174,7 @@ def main():
         'config': {
             'workload': 'C3: CONUS ARD tile chips (100x100 px, L4-L8 1982-2017 cadence, %d obs/pixel), %d chips per GPU per step' % (n_obs, len(ids)),
             'synthetic_config': args.config,
-            'chips_per_gpu': len(ids),
+            'chips_per_gpu': len(ids), 'contexts_per_gpu': len(ctxs),
             'pixels_per_chip': PIXELS_PER_CHIP,
             'n_obs': n_obs,
             'tile_chips': TILE_CHIPS,
@@ -169,9 +191,10 @@ def main():
             'kernel': {'w1': 'ccd_detect', 'w2': 'ccd_detect_w2'}.get(os.environ.get('CCDGPU_KERNEL', 'w3'), 'ccd_detect_w3'),
             'traffic_note': 'traffic = HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE (profiles/pmc_detect.json); mostly per-wave scratch (compacted period, closest-DOY buckets) re-read from HBM',
             'kernel_ms_per_launch': det_avg,
+            'launch_ms_effective': launch_ms,
             'flops_per_launch': flops,
             'algorithmic_bytes_per_launch': alg_bytes,
-            'algorithmic_hbm_gbs': alg_bytes / (det_avg * 1e-3) / 1e9,
+            'algorithmic_hbm_gbs': alg_bytes / (launch_ms * 1e-3) / 1e9,
             'hbm_peak_gbs': HBM_PEAK_GBS,
         },
         'segments_per_step': segs * world,

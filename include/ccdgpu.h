@@ -127,7 +127,10 @@ const char *ccdgpu_version(void);
 const char *ccdgpu_last_error(void);
 void ccdgpu_params_default(ccdgpu_params *p);
 
-/* Create a context bound to HIP device `device` (one context per device and host thread). */
+/* Create a context bound to HIP device `device`.  A context is used by one host thread at a
+ * time; up to 16 contexts may live in a process, and contexts on the same device run their
+ * detections concurrently (each has its own stream, buffers and launch-argument slot), so a
+ * second context's launch fills the CUs the first one's launch tail leaves idle. */
 int ccdgpu_init(int device, ccdgpu_ctx **ctx);
 int ccdgpu_destroy(ccdgpu_ctx *ctx);
 int ccdgpu_device_count(int *count);

@@ -22,6 +22,8 @@
 #define CCD_NB 7
 #define CCD_WAVE 64
 #define CCD_BASIS_STRIDE 8
+// launch-argument slots in constant memory: contexts of one process that can run at once
+#define CCD_ARG_SLOTS 16
 
 struct CcdDetectArgs {
     ccdgpu_params p;
@@ -62,10 +64,10 @@ extern "C" {
 // kernel launchers (ccd_kernels.hip)
 int ccdk_prep(const int64_t *dates, int32_t n_chips, int32_t n_obs, double avg_days_yr,
               int32_t *order, int64_t *sdates, double *basis, void *stream);
-// the detection kernel reads its arguments from a __constant__ symbol (one staged launch per
-// device at a time; the host API serialises launches per device)
-int ccdk_set_args(const CcdDetectArgs *host_args, void *stream);
-int ccdk_detect(int32_t grid, int variant, int32_t n_obs, void *stream);
+// the detection kernel reads its arguments from slot arg_slot of a __constant__ array (one slot
+// per live context, so contexts on one device may launch concurrently from their own streams)
+int ccdk_set_args(const CcdDetectArgs *host_args, int arg_slot, void *stream);
+int ccdk_detect(int32_t grid, int variant, int32_t n_obs, int arg_slot, void *stream);
 // 1 if this build keeps the compacted period in LDS (-DCCD_PERIOD_IN_LDS)
 int ccdk_period_in_lds(void);
 // dynamic LDS bytes per wave and resident waves per CU for a period of n_obs observations

@@ -77,17 +77,19 @@ struct __attribute__((aligned(16))) Lds {
     };
 };
 
-// Launch arguments live in constant memory (uniform scalar loads from every device function);
-// the per-wave LDS block is the dynamic shared segment (so every access is a ds_* instruction).
-__constant__ CcdDetectArgs c_args;
-// Every device function reads the launch arguments through ARGS(): the opaque zero index keeps
-// the compiler from hoisting the (invariant) constant loads to the top of the persistent kernel,
-// where they would stay live in SGPRs for its whole length and be spilled; re-reading them at
-// the use is a scalar-cache hit.
+// Launch arguments live in constant memory (uniform scalar loads from every device function),
+// one slot per host context so that contexts sharing a device can run concurrently; the launch
+// passes its slot as the kernel's only argument.  The per-wave LDS block is the dynamic shared
+// segment (so every access is a ds_* instruction).
+__constant__ CcdDetectArgs c_args[CCD_ARG_SLOTS];
+// Every device function reads the launch arguments through ARGS(): the slot index is read from
+// the kernel-argument segment and made opaque, which keeps the compiler from hoisting the
+// (invariant) constant loads to the top of the persistent kernel, where they would stay live in
+// SGPRs for its whole length and be spilled; re-reading them at the use is a scalar-cache hit.
 __device__ __forceinline__ const CcdDetectArgs &ARGS() {
-    int z = 0;
+    int z = *(const int *)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(z));
-    return (&c_args)[z];
+    return c_args[z];
 }
 extern __shared__ __attribute__((aligned(16))) char ccd_smem[];
 __device__ __forceinline__ Lds &LDS() { return *reinterpret_cast<Lds *>(ccd_smem); }
@@ -2776,10 +2778,11 @@ __device__ __forceinline__ void detect_body() {
 // 168 VGPRs, some spills).  The host picks one (CCDGPU_KERNEL=w1|w2|w3; default w3, the fastest).
 // A 4-waves/SIMD build (128 VGPRs) was dropped: its code generation broke golden parity
 // (deterministically, on every golden case), while w1..w3 of the same source match.
-__global__ __launch_bounds__(64) __attribute__((flatten)) void ccd_detect() { detect_body(); }
-__global__ __launch_bounds__(64, 2) __attribute__((flatten)) void ccd_detect_w2() { detect_body(); }
-__global__ __launch_bounds__(64, 3) __attribute__((flatten)) void ccd_detect_w3() { detect_body(); }
-__global__ __launch_bounds__(64, 4) __attribute__((flatten)) void ccd_detect_w4() { detect_body(); }
+// (arg_slot: the c_args slot of the launching context, read by ARGS() from the kernarg segment)
+__global__ __launch_bounds__(64) __attribute__((flatten)) void ccd_detect(int arg_slot) { detect_body(); }
+__global__ __launch_bounds__(64, 2) __attribute__((flatten)) void ccd_detect_w2(int arg_slot) { detect_body(); }
+__global__ __launch_bounds__(64, 3) __attribute__((flatten)) void ccd_detect_w3(int arg_slot) { detect_body(); }
+__global__ __launch_bounds__(64, 4) __attribute__((flatten)) void ccd_detect_w4(int arg_slot) { detect_body(); }
 
 // ------------------------------------------------------------------ per-chip preparation
 // One 256-thread block per chip: stable rank of each date (ties by input position), sorted
@@ -2845,8 +2848,9 @@ extern "C" int ccdk_prep(const int64_t *dates, int32_t n_chips, int32_t n_obs, d
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-extern "C" int ccdk_set_args(const CcdDetectArgs *host_args, void *stream) {
-    return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_args), host_args, sizeof(CcdDetectArgs), 0,
+extern "C" int ccdk_set_args(const CcdDetectArgs *host_args, int arg_slot, void *stream) {
+    if (arg_slot < 0 || arg_slot >= CCD_ARG_SLOTS) return -1;
+    return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_args), host_args, sizeof(CcdDetectArgs), sizeof(CcdDetectArgs) * (size_t)arg_slot,
                                   hipMemcpyHostToDevice, (hipStream_t)stream) == hipSuccess ? 0 : -1;
 }
 
@@ -2886,13 +2890,14 @@ extern "C" int ccdk_occupancy(int variant, int32_t n_obs) {
     return blocks;
 }
 
-extern "C" int ccdk_detect(int32_t grid, int variant, int32_t n_obs, void *stream) {
+extern "C" int ccdk_detect(int32_t grid, int variant, int32_t n_obs, int arg_slot, void *stream) {
     const size_t lds = ccdk_lds_bytes(n_obs);
+    if (arg_slot < 0 || arg_slot >= CCD_ARG_SLOTS) return -1;
     switch (variant) {
-    case 1: hipLaunchKernelGGL(ccd_detect, dim3(grid), dim3(64), lds, (hipStream_t)stream); break;
-    case 2: hipLaunchKernelGGL(ccd_detect_w2, dim3(grid), dim3(64), lds, (hipStream_t)stream); break;
-    case 4: hipLaunchKernelGGL(ccd_detect_w4, dim3(grid), dim3(64), lds, (hipStream_t)stream); break;
-    default: hipLaunchKernelGGL(ccd_detect_w3, dim3(grid), dim3(64), lds, (hipStream_t)stream); break;
+    case 1: hipLaunchKernelGGL(ccd_detect, dim3(grid), dim3(64), lds, (hipStream_t)stream, arg_slot); break;
+    case 2: hipLaunchKernelGGL(ccd_detect_w2, dim3(grid), dim3(64), lds, (hipStream_t)stream, arg_slot); break;
+    case 4: hipLaunchKernelGGL(ccd_detect_w4, dim3(grid), dim3(64), lds, (hipStream_t)stream, arg_slot); break;
+    default: hipLaunchKernelGGL(ccd_detect_w3, dim3(grid), dim3(64), lds, (hipStream_t)stream, arg_slot); break;
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

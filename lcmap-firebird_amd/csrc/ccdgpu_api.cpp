@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -75,13 +76,32 @@ double chi2_5_ppf(double p) {
     return 0.5 * (lo + hi);
 }
 
+// constant-memory launch-argument slots (CCD_ARG_SLOTS per process): one per live context
+std::mutex g_slot_mu;
+unsigned g_slots_used = 0;
+int acquire_arg_slot() {
+    std::lock_guard<std::mutex> g(g_slot_mu);
+    for (int i = 0; i < CCD_ARG_SLOTS; ++i)
+        if (!(g_slots_used & (1u << i))) {
+            g_slots_used |= 1u << i;
+            return i;
+        }
+    return -1;
+}
+void release_arg_slot(int i) {
+    if (i < 0) return;
+    std::lock_guard<std::mutex> g(g_slot_mu);
+    g_slots_used &= ~(1u << i);
+}
+
 }  // namespace
 
 struct ccdgpu_ctx {
     int device = 0;
     int n_cu = 0;
     int slots_per_cu = 0;
-    int variant = 3;  // detection kernel register budget: 1..3 waves/SIMD (CCDGPU_KERNEL=w1..w3)
+    int variant = 3;  // detection kernel register budget: 1..4 waves/SIMD (CCDGPU_KERNEL=w1..w4)
+    int arg_slot = -1;  // this context's launch-argument slot in constant memory
     hipStream_t stream = nullptr;
     hipStream_t copy_stream = nullptr;  // uploads of ccdgpu_stage_slot (overlap a running detection)
     hipEvent_t uploaded[2] = {nullptr, nullptr};
@@ -152,6 +172,7 @@ struct ccdgpu_ctx {
         for (auto &e : ev)
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
+        release_arg_slot(arg_slot);
     }
 };
 
@@ -247,6 +268,11 @@ int ccdgpu_init(int device, ccdgpu_ctx **out) {
         return fail(CCDGPU_EHIP, "hipStreamCreate failed");
     }
     for (auto &e : c->uploaded) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    c->arg_slot = acquire_arg_slot();
+    if (c->arg_slot < 0) {
+        delete c;
+        return fail(CCDGPU_EINVAL, "more than " + std::to_string(CCD_ARG_SLOTS) + " live contexts in this process");
+    }
     c->slots_per_cu = 16;
     c->variant = ccdk_period_in_lds() ? 1 : 3;
     if (const char *v = std::getenv("CCDGPU_KERNEL")) {
@@ -495,12 +521,12 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         unsigned long long init[8] = {0ull, 0ull, ~0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
         HIPCHK(hipMemcpyAsync(c->counters.p, init, sizeof(init), hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipMemsetAsync(c->stats.p, 0, sizeof(unsigned long long) * CCD_NSTATS, c->stream));
-        if (ccdk_set_args(&a, c->stream)) return fail(CCDGPU_EHIP, "copying kernel arguments to constant memory failed");
+        if (ccdk_set_args(&a, c->arg_slot, c->stream)) return fail(CCDGPU_EHIP, "copying kernel arguments to constant memory failed");
         HIPCHK(hipEventRecord(c->ev[0], c->stream));
         if (ccdk_prep(c->in_dates, c->n_chips, c->n_obs, p.avg_days_yr, c->order.p, c->sdates.p, c->basis.p, c->stream))
             return fail(CCDGPU_EHIP, std::string("prep launch: ") + hipGetErrorString(hipGetLastError()));
         HIPCHK(hipEventRecord(c->ev[1], c->stream));
-        if (ccdk_detect(c->n_slots, c->variant, c->n_obs, c->stream))
+        if (ccdk_detect(c->n_slots, c->variant, c->n_obs, c->arg_slot, c->stream))
             return fail(CCDGPU_EHIP, std::string("detect launch: ") + hipGetErrorString(hipGetLastError()));
         HIPCHK(hipEventRecord(c->ev[2], c->stream));
         unsigned long long h[8];

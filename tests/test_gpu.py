@@ -189,3 +189,33 @@ def test_upload_slots_match_staged_path(ctx):
         assert np.array_equal(got.seg_offsets, ref[i].seg_offsets)
         assert got.segments.tobytes() == ref[i].segments.tobytes()
         assert np.array_equal(got.mask, ref[i].mask)
+
+
+def test_concurrent_contexts_on_one_device():
+    """Two contexts on one device detecting from two host threads at once (own streams, buffers
+    and launch-argument slots) give the same results as one context alone."""
+    import threading
+    batches = [synth.chip(synth.config(c), 7, 0, 1500) for c in (2, 5)]
+    ref = []
+    solo = ccdgpu.Context(0)
+    for d, s, q in batches:
+        ref.append(solo.detect_batch(d, s, q))
+    solo.close()
+    ctxs = [ccdgpu.Context(0), ccdgpu.Context(0)]
+    got = [None, None]
+
+    def work(i):
+        for _ in range(3):
+            got[i] = ctxs[i].detect_batch(*batches[i])
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for c in ctxs:
+        c.close()
+    for g, r in zip(got, ref):
+        assert np.array_equal(g.seg_offsets, r.seg_offsets)
+        assert g.segments.tobytes() == r.segments.tobytes()
+        assert np.array_equal(g.mask, r.mask)
