@@ -44,7 +44,7 @@ def parse():
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--chips', type=int, default=64, help='chips per GPU per step')
     ap.add_argument('--config', type=int, default=3, help='synthetic config (2, 3, 4 or 5)')
-    ap.add_argument('--contexts', type=int, default=2,
+    ap.add_argument('--contexts', type=int, default=1,
                     help='contexts per GPU running steps concurrently (each stages the same chips)')
     ap.add_argument('--cpu-seconds', type=float, default=12.0, help='target CPU-baseline sample time')
     ap.add_argument('--cpu-threads', type=int, default=16)
