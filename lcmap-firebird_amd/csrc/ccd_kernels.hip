@@ -947,10 +947,12 @@ __device__ __forceinline__ void variogram(Px &P) {
     int small[NB];
 #pragma unroll
     for (int band = 0; band < NB; ++band) small[band] = 0;
-    constexpr int U = 2;  // two chunks per round, loads before the stores
-    for (int base0 = 0; base0 < m - kk; base0 += U * W) {
-        bool okv[U];
-        uint4 r0v[U], r1v[U];
+    // two chunks per round, loads before the stores; the next round's loads go out before this
+    // round's stores
+    constexpr int U = 2;
+    bool okn[U];
+    uint4 r0n[U], r1n[U];
+    auto load = [&](int base0, bool (&okv)[U], uint4 (&r0v)[U], uint4 (&r1v)[U]) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int i = base0 + u * W + l;
@@ -963,6 +965,18 @@ __device__ __forceinline__ void variogram(Px &P) {
                 r1v[u] = reinterpret_cast<const uint4 *>(PCR(P))[i + kk];
             }
         }
+    };
+    load(0, okn, r0n, r1n);
+    for (int base0 = 0; base0 < m - kk; base0 += U * W) {
+        bool okv[U];
+        uint4 r0v[U], r1v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            okv[u] = okn[u];
+            r0v[u] = r0n[u];
+            r1v[u] = r1n[u];
+        }
+        load(base0 + U * W, okn, r0n, r1n);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const bool ok = okv[u];
