@@ -202,6 +202,9 @@ typedef struct ccdgpu_stats {
     int64_t cd_sweeps;          /* coordinate-descent sweeps summed over fits              */
     int64_t flops;              /* counted FP64 flops (SURVEY.md §8(d) op-count model)     */
     int64_t bytes;              /* algorithmic HBM bytes read+written                      */
+    double detect_ms_device;    /* the detection kernel's execution window, first wave in to
+                                   last wave out, on the device's 100 MHz clock (excludes time
+                                   queued behind another context's launch)                 */
 } ccdgpu_stats;
 int ccdgpu_last_stats(ccdgpu_ctx *ctx, ccdgpu_stats *stats);
 

@@ -114,7 +114,8 @@ class Result(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [('detect_ms', _f64), ('prep_ms', _f64), ('pixels', ctypes.c_int64),
                 ('segments', ctypes.c_int64), ('lasso_fits', ctypes.c_int64),
-                ('cd_sweeps', ctypes.c_int64), ('flops', ctypes.c_int64), ('bytes', ctypes.c_int64)]
+                ('cd_sweeps', ctypes.c_int64), ('flops', ctypes.c_int64), ('bytes', ctypes.c_int64),
+                ('detect_ms_device', _f64)]
 
 
 # parameter dict keys (pyccd parameters.yaml names) -> Params fields

@@ -38,7 +38,8 @@ struct CcdDetectArgs {
     const int64_t *sdates;
     const double *basis;
     // work queue + global flags: [0] next pixel, [1] pool count, [2] first QA-error pixel (min),
-    // [3] pool overflow, [4] first source line whose index guard tripped (0 = none)
+    // [3] pool overflow, [4] first source line whose index guard tripped (0 = none),
+    // [5] / [6] s_memrealtime of the first wave's start / the last wave's end (100 MHz)
     unsigned long long *counters;
     // per-slot scratch
     int32_t *s_date;

@@ -2720,6 +2720,9 @@ __device__ __forceinline__ void detect_body() {
 #ifdef CCD_PHASE_TIMERS
     if (l < CCD_NPHASE) lds.tph[l] = 0;
 #endif
+    // launch execution window on the device's constant-rate clock (first wave in, last wave out):
+    // the kernel's own duration even when it queued behind another context's launch
+    if (l == 0) atomicMin(&A.counters[5], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     for (;;) {
         unsigned long long job = 0;
         if (l == 0) job = atomicAdd(&A.counters[0], 1ull);
@@ -2773,6 +2776,7 @@ __device__ __forceinline__ void detect_body() {
         if (l == 0 && bl) atomicCAS(&A.counters[4], 0ull, (unsigned long long)bl);
     }
     // instrumentation
+    if (l == 0) atomicMax(&A.counters[6], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     unsigned long long sw = P.sweeps, fll = P.fl_lane;
     for (int o = 32; o > 0; o >>= 1) {
         sw += __shfl_xor(sw, o);
@@ -2788,10 +2792,9 @@ __device__ __forceinline__ void detect_body() {
     }
 }
 
-// Three register budgets of the same body: 1 wave/SIMD (no spills), 2 and 3 waves/SIMD (256 and
-// 168 VGPRs, some spills).  The host picks one (CCDGPU_KERNEL=w1|w2|w3; default w3, the fastest).
-// A 4-waves/SIMD build (128 VGPRs) was dropped: its code generation broke golden parity
-// (deterministically, on every golden case), while w1..w3 of the same source match.
+// Four register budgets of the same body: 1 wave/SIMD (no spills), 2, 3 and 4 waves/SIMD (256,
+// 168 and 128 VGPRs, spills growing).  The host picks one (CCDGPU_KERNEL=w1..w4; default w3, the
+// fastest: w4's spills cost more than its 4th wave gains).
 // (arg_slot: the c_args slot of the launching context, read by ARGS() from the kernarg segment)
 __global__ __launch_bounds__(64) __attribute__((flatten)) void ccd_detect(int arg_slot) { detect_body(); }
 __global__ __launch_bounds__(64, 2) __attribute__((flatten)) void ccd_detect_w2(int arg_slot) { detect_body(); }

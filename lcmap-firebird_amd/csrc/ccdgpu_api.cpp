@@ -518,7 +518,7 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         a.pool = c->pool.p;
         a.pool_seq = c->pool_seq.p;
         a.pool_cap = c->pool_cap;
-        unsigned long long init[8] = {0ull, 0ull, ~0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
+        unsigned long long init[8] = {0ull, 0ull, ~0ull, 0ull, 0ull, ~0ull, 0ull, 0ull};
         HIPCHK(hipMemcpyAsync(c->counters.p, init, sizeof(init), hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipMemsetAsync(c->stats.p, 0, sizeof(unsigned long long) * CCD_NSTATS, c->stream));
         if (ccdk_set_args(&a, c->arg_slot, c->stream)) return fail(CCDGPU_EHIP, "copying kernel arguments to constant memory failed");
@@ -563,6 +563,7 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         HIPCHK(hipEventRecord(c->ev[3], c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         c->last.detect_ms = ms_det;
+        c->last.detect_ms_device = h[6] > h[5] ? (double)(h[6] - h[5]) / 1e5 : 0.0;  // 100 MHz clock
         c->last.prep_ms = ms_prep;
         c->last.pixels = c->total_pix;
         c->last.segments = c->n_pool;
