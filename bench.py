@@ -51,6 +51,8 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-packer', action='store_true', help='skip the chip-packer (chipmunk decode) leg')
     ap.add_argument('--no-stream', action='store_true', help='skip the end-to-end (PCIe-inclusive) streaming leg')
+    ap.add_argument('--share-device', action='store_true',
+                    help='rehearsal only: ranks beyond the device count share devices (LOCAL_RANK mod count)')
     return ap.parse_args()
 
 
@@ -94,7 +96,11 @@ def main():
         assert np.array_equal(d, dates)
         D[j], S[j], Q[j] = d, s, q
 
-    ctxs = [ccdgpu.Context(local) for _ in range(max(1, args.contexts))]
+    ndev = ccdgpu.device_count()
+    if local >= ndev and not args.share_device:
+        raise SystemExit('LOCAL_RANK %d but only %d device(s) visible' % (local, ndev))
+    device = local % ndev
+    ctxs = [ccdgpu.Context(device) for _ in range(max(1, args.contexts))]
     for c in ctxs:
         c.stage(D, S, Q)
     ctx = ctxs[0]
