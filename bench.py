@@ -77,7 +77,12 @@ def main():
     if world != args.gpus and 'WORLD_SIZE' in os.environ:
         print('warning: --gpus %d but WORLD_SIZE %d' % (args.gpus, world), file=sys.stderr)
     dist = None
+    json_out = sys.stdout
     if world > 1:
+        # gloo's native connection log goes to fd 1; keep stdout for the one JSON line
+        sys.stdout.flush()
+        json_out = os.fdopen(os.dup(1), 'w')
+        os.dup2(2, 1)
         import torch.distributed as dist
         dist.init_process_group('gloo', rank=rank, world_size=world)
 
@@ -220,7 +225,7 @@ def main():
         out['cpu_baseline'] = cpu_baseline(S[0], Q[0], dates, args)
         out['speedup_vs_cpu_baseline'] = value / out['cpu_baseline']['value']
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
