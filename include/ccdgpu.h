@@ -27,11 +27,15 @@ extern "C" {
 #define CCDGPU_EHIP (-2)     /* HIP runtime error (no device, launch failure, ...)     */
 #define CCDGPU_EQA (-3)      /* unsupported bit-packed QA value (pyccd ValueError)     */
 #define CCDGPU_ENOMEM (-4)   /* device or host allocation failed                       */
-#define CCDGPU_EOVERFLOW (-5)/* internal capacity exceeded (segments per pixel, peek)  */
+#define CCDGPU_EOVERFLOW (-5)/* capacity exceeded (adaptive peek > CCDGPU_MAX_PEEK)    */
 
 #define CCDGPU_NBANDS 7      /* blue, green, red, nir, swir1, swir2, thermal            */
 #define CCDGPU_MAX_OBS 4096  /* observations per pixel the kernels accept              */
-#define CCDGPU_MAX_PEEK 64   /* largest (adaptive) look-ahead window                     */
+/* Largest (adaptive) look-ahead window.  The ncompare peek is round(16 PEEK_SIZE / median gap)
+ * over the filtered, duplicate-free dates, so with the default PEEK_SIZE 6 it never exceeds 96
+ * (median gap >= 1 day): every default-parameter pixel is supported.  A configured PEEK_SIZE > 6
+ * can push it past 96 on dense dates; that pixel fails the call with CCDGPU_EOVERFLOW. */
+#define CCDGPU_MAX_PEEK 96
 
 /* ccd/parameters.yaml defaults; ccdgpu_params_default() fills them. */
 typedef struct ccdgpu_params {
@@ -146,10 +150,20 @@ int ccdgpu_detect_batch(ccdgpu_ctx *ctx, const ccdgpu_params *params, int32_t n_
                         ccdgpu_result *out);
 void ccdgpu_result_free(ccdgpu_result *out);
 
-/* Device-resident path (benchmarks, multi-chip pipelines): stage a batch once, run the
- * detection as often as wanted on the resident copy, fetch results separately.  Up to
- * `n_chips` chips of identical (n_pix, n_obs) shape are staged back to back; chip c's arrays
- * start at c * n_obs / c * 7 * n_pix * n_obs / c * n_pix * n_obs elements of the host buffers. */
+/* Device-resident path (tile runner, benchmarks, batched Spark partitions): stage a batch once,
+ * run the detection as often as wanted on the resident copy, fetch results separately.
+ *
+ * A batch is `n_chips` chips -- pixel groups that share one date vector, as merlin builds them
+ * per chip (ccdc/timeseries.py:107-115) -- with their own sizes: chip c has n_pix[c] pixels and
+ * n_obs[c] observations, so a tile's base-cadence and sidelap chips (and the date groups of a
+ * Spark partition) run in one launch.  Their arrays are packed back to back:
+ *   dates   chip c at  O_c = sum_{c' < c} n_obs[c']               [n_obs[c]]
+ *   spectra chip c at  7 * D_c, D_c = sum_{c' < c} n_pix[c'] n_obs[c']   [7][n_pix[c]][n_obs[c]]
+ *   qa      chip c at  D_c                                          [n_pix[c]][n_obs[c]]
+ * Pixel p of the batch is pixel p - sum_{c' < c} n_pix[c'] of chip c. */
+int ccdgpu_stage_chips(ccdgpu_ctx *ctx, const ccdgpu_params *params, int32_t n_chips, const int32_t *n_pix,
+                       const int32_t *n_obs, const int64_t *dates, const int16_t *spectra, const uint16_t *qa);
+/* ccdgpu_stage_chips with every chip of shape (n_pix, n_obs). */
 int ccdgpu_stage(ccdgpu_ctx *ctx, const ccdgpu_params *params, int32_t n_chips, int32_t n_pix,
                  int32_t n_obs, const int64_t *dates, const int16_t *spectra, const uint16_t *qa);
 int ccdgpu_run_staged(ccdgpu_ctx *ctx, double *kernel_seconds);
@@ -174,22 +188,30 @@ int ccdgpu_stage_chipmunk(ccdgpu_ctx *ctx, const ccdgpu_params *params, int32_t 
  * streaming loop  stage_slot(0, b0); for i: { stage_slot((i+1)&1, b_{i+1}); run_slot(i&1); fetch }
  * overlaps each upload with the previous batch's detection.  Host inputs must stay valid and
  * unchanged until the run_slot of their slot returns; they should be pinned (ccdgpu_host_alloc),
- * or the upload is synchronous.  Batches of both slots need the same params. */
+ * or the upload is synchronous.  Each slot keeps the params it was staged with. */
 int ccdgpu_host_alloc(size_t bytes, void **ptr);
 int ccdgpu_host_free(void *ptr);
+int ccdgpu_stage_slot_chips(ccdgpu_ctx *ctx, int32_t slot, const ccdgpu_params *params, int32_t n_chips,
+                            const int32_t *n_pix, const int32_t *n_obs, const int64_t *dates, const int16_t *spectra,
+                            const uint16_t *qa);
 int ccdgpu_stage_slot(ccdgpu_ctx *ctx, int32_t slot, const ccdgpu_params *params, int32_t n_chips, int32_t n_pix,
                       int32_t n_obs, const int64_t *dates, const int16_t *spectra, const uint16_t *qa);
 int ccdgpu_run_slot(ccdgpu_ctx *ctx, int32_t slot, double *kernel_seconds);
 
-/* Copy the staged pixel inputs back to the host in the ccdgpu_stage layout (spectra
- * [n_chips][7][n_pix][n_obs], qa [n_chips][n_pix][n_obs]); either pointer may be NULL. */
+/* Copy the staged pixel inputs back to the host in the ccdgpu_stage_chips layout; either
+ * pointer may be NULL. */
 int ccdgpu_staged_inputs(ccdgpu_ctx *ctx, int16_t *spectra, uint16_t *qa);
+/* CSR result of staged chip `chip` (n_pix / n_obs of that chip). */
 int ccdgpu_fetch_staged(ccdgpu_ctx *ctx, int32_t chip, ccdgpu_result *out);
 
 /* Output writer: the segment / pixel table rows of staged chip `chip` of the last run, packed on
  * the device (ccd_rows.hip) for the chip at (cx, cy) with `width` pixels per chip row (100).
  * Replaces the per-segment Python formatting of ccdc/pyccd.py:106-148 + Spark's float cast. */
 int ccdgpu_fetch_rows(ccdgpu_ctx *ctx, int32_t chip, int32_t cx, int32_t cy, int32_t width, ccdgpu_rows *out);
+/* The same for every chip of the batch in one device pass and one copy (the tile runner's
+ * gather): chip c at (cx[c], cy[c]); row_offsets over all pixels of the batch; mask of chip c
+ * at byte D_c (ccdgpu_stage_chips), [n_pix[c]][n_obs[c]]; out->n_obs is 0 for a multi-chip batch. */
+int ccdgpu_fetch_batch_rows(ccdgpu_ctx *ctx, const int32_t *cx, const int32_t *cy, int32_t width, ccdgpu_rows *out);
 void ccdgpu_rows_free(ccdgpu_rows *out);
 
 /* Kernel statistics of the last run (per launch of the main detection kernel). */

@@ -6,8 +6,9 @@ The reference binds pyccd in exactly two places (ccdc/pyccd.py):
                                                            test/__init__.py:37-46)
 ``detect`` keeps pyccd's signature, argument meaning and error behaviour (AssertionError on
 mismatched shapes like pyccd's __check_inputs, ValueError on an unsupported bit-packed QA value
-like qa.qabitval) and returns pyccd's result dict.  ``detect_batch`` is the batched entry the
-Spark ``mapPartitions`` path uses: pixels that share a date vector go to the GPU in one call.
+like qa.qabitval) and returns pyccd's result dict.  ``detect_batch`` / ``detect_records`` are
+the batched entries the Spark ``mapPartitions`` path uses: a partition's pixels, grouped by date
+vector, go to the GPU in one launch.
 Every call runs on the GPU through libccdgpu.so; there is no CPU fallback.
 """
 import numpy as np
@@ -65,14 +66,37 @@ def detect_batch(dates, spectra, qas, params=None):
     return [abi.pixel_result(u, px, algorithm) for px in range(n_pix)]
 
 
+def detect_groups(groups, params=None):
+    """[(dates [n], spectra [7][n_pix][n], qas [n_pix][n]), ...] -- pixel groups with their own
+    date vectors -- -> [[result per pixel] per group], all groups in ONE device launch
+    (ccdgpu_stage_chips: groups of their own sizes back to back).  Raises ValueError
+    (QAValueError) if any pixel has an unsupported QA value."""
+    out = [None] * len(groups)
+    live = [i for i, g in enumerate(groups) if np.asarray(g[0]).shape[0] > 0]
+    for i, g in enumerate(groups):
+        if i not in live:
+            out[i] = [_empty_result(0) for _ in range(np.asarray(g[2]).shape[0])]
+    if live:
+        ctx = ccdgpu.default_context()
+        ctx.stage_chips([groups[i] for i in live], params)
+        ctx.run()
+        for c, i in enumerate(live):
+            u = ctx.fetch(c)
+            if u.error_pixel >= 0:
+                raise ccdgpu.QAValueError('unsupported bit-packed QA value (group %d, pixel %d)' % (i, u.error_pixel))
+            out[i] = [abi.pixel_result(u, px, algorithm) for px in range(u.n_pix)]
+    return out
+
+
 def detect_records(records, params=None):
-    """[(key, {dates, blues..thermals, qas}), ...] -> [(key, result), ...], batching records
-    that share a date vector (a chip's pixels, as merlin.create builds them) into one GPU call."""
+    """[(key, {dates, blues..thermals, qas}), ...] -> [(key, result), ...].  Records are grouped
+    by date vector (a chip's pixels, as merlin.create builds them) and every group of the call
+    runs in one device launch (detect_groups)."""
     groups = {}
     for idx, (key, rec) in enumerate(records):
         d = np.asarray(rec['dates'], dtype=np.int64)
         groups.setdefault(d.tobytes(), (d, []))[1].append((idx, key, rec))
-    out = [None] * len(records)
+    arrays, members_of = [], []
     for d, members in groups.values():
         n = d.shape[0]
         spectra = np.empty((7, len(members), n), dtype=np.int16)
@@ -81,7 +105,10 @@ def detect_records(records, params=None):
             for b, kw in enumerate(BAND_KWARGS):
                 spectra[b, j] = rec[kw]
             qas[j] = rec['qas']
-        results = detect_batch(d, spectra, qas, params)
+        arrays.append((d, spectra, qas))
+        members_of.append(members)
+    out = [None] * len(records)
+    for members, results in zip(members_of, detect_groups(arrays, params)):
         for (idx, key, _), res in zip(members, results):
             out[idx] = (key, res)
     return out

@@ -203,20 +203,22 @@ def detect_partition(records, params=None):
     return rows
 
 
-def _run_chips(chips, params, context):
+def _run_chips(chips, params, context, symmetric=True):
     """Group chipmunk chips by location, batch locations that share a date vector, stage each
     batch with the device chip packer and detect it.  Yields (ctx, chip index, (cx, cy),
-    dates [n] int64 descending, n_pix) for every location, batch by batch."""
+    dates [n] int64 descending, n_pix) for every location, batch by batch.  symmetric=False
+    accepts locations whose layers lack some dates (they stage as fill, QA 1) instead of
+    raising like merlin's symmetric date check."""
     import ccdgpu
     from ccdc import chipmunk
     groups = chipmunk.group(chips)
     ctx = context or ccdgpu.default_context()
     batches = {}
     for key, layers in groups.items():
-        d = chipmunk.dates_of(layers)
+        d = chipmunk.dates_of(layers, symmetric)
         batches.setdefault(d.tobytes(), []).append((key, layers))
     for members in batches.values():
-        dates, text, offsets = chipmunk.pack_text([layers for _, layers in members])
+        dates, text, offsets = chipmunk.pack_text([layers for _, layers in members], symmetric)
         first_payload = next(v for _, layers in members for n in chipmunk.LAYERS for v in layers[n].values())
         n_pix = chipmunk.payload_pixels(first_payload)
         ctx.stage_chipmunk(dates, text, offsets, n_pix, params)
@@ -225,20 +227,20 @@ def _run_chips(chips, params, context):
             yield ctx, c, key, dates[0], n_pix
 
 
-def detect_chips(chips, params=None, context=None):
+def detect_chips(chips, params=None, context=None, symmetric=True):
     """Change detection straight from chipmunk chips (the wire format merlin.create consumes in
     timeseries.rdd, timeseries.py:120): chips of any number of locations, grouped by location,
     batched by shared date vector, decoded and pivoted on the device (ccdc.chipmunk,
     ccdgpu.Context.stage_chipmunk) and detected there.  Returns the rows ``detect`` would give
     for every pixel of every location (pixel keys as test/__init__.py:37: px = cx + 30 col,
     py = cy - 30 row), locations in first-seen order.  Raises ValueError (QAValueError) on an
-    unsupported QA value, like ccd.detect."""
+    unsupported QA value, like ccd.detect.  symmetric: see _run_chips."""
     import ccdgpu
     from ccdgpu import abi
     from ccdc import timeseries
     rows = {}
     order = []
-    for ctx, c, (cx, cy), dates, n_pix in _run_chips(chips, params, context):
+    for ctx, c, (cx, cy), dates, n_pix in _run_chips(chips, params, context, symmetric):
         u = ctx.fetch(c)
         if u.error_pixel >= 0:
             raise ccdgpu.QAValueError('unsupported QA value at pixel %d of chip (%d, %d)' % (u.error_pixel, cx, cy))

@@ -8,7 +8,9 @@ types (``ccdgpu.Context.fetch_rows``: float32, one byte per mask entry, ccd_rows
 assembled column-wise into Arrow tables whose column names and types follow the reference
 schemas exactly; ``write_parquet`` is the offline sink (the Cassandra writer stays out of scope,
 SURVEY.md §2).  A pixel without change models keeps pyccd.default's day-1 row with every band,
-chprob and curqa column null, as in the reference.
+chprob and curqa column null, as in the reference.  A model with break_day 0 (the single fit of
+the permanent-snow and insufficient-clear procedures) is written with a null bday -- the one
+deliberate difference: the reference's format raises ValueError on that row.
 """
 import os
 
@@ -66,7 +68,10 @@ def _row_columns(cx, cy, rows):
         'cx': pa.array(np.full(n, cx, np.int32)), 'cy': pa.array(np.full(n, cy, np.int32)),
         'px': pa.array(rows['px']), 'py': pa.array(rows['py']),
         'sday': pa.array(iso_days(rows['sday'])), 'eday': pa.array(iso_days(rows['eday'])),
-        'bday': pa.array(iso_days(rows['bday'])),
+        # break_day 0 (permanent-snow / insufficient-clear models have no break): null bday.
+        # The reference's pyccd.format would raise in date.fromordinal(0) on such a row
+        # (SURVEY.md §7 edge (a)); the bday column is nullable in its schema (pyccd.py:46).
+        'bday': pa.array(iso_days(np.maximum(rows['bday'], 1)), mask=rows['bday'] < 1),
         'chprob': _float_col(rows['chprob'], valid),
         'curqa': pa.array(rows['curqa'].astype(np.int32), mask=~valid),
     }

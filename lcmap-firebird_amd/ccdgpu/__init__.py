@@ -45,6 +45,11 @@ def _declare(L):
     L.ccdgpu_result_free.argtypes = [c.POINTER(abi.Result)]
     L.ccdgpu_stage.argtypes = [c.c_void_p, c.POINTER(abi.Params), c.c_int32, c.c_int32, c.c_int32,
                                c.c_void_p, c.c_void_p, c.c_void_p]
+    L.ccdgpu_stage_chips.argtypes = [c.c_void_p, c.POINTER(abi.Params), c.c_int32, c.c_void_p, c.c_void_p,
+                                     c.c_void_p, c.c_void_p, c.c_void_p]
+    L.ccdgpu_stage_slot_chips.argtypes = [c.c_void_p, c.c_int32, c.POINTER(abi.Params), c.c_int32, c.c_void_p,
+                                          c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p]
+    L.ccdgpu_fetch_batch_rows.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_int32, c.POINTER(abi.Rows)]
     L.ccdgpu_stage_chipmunk.argtypes = [c.c_void_p, c.POINTER(abi.Params), c.c_int32, c.c_int32, c.c_int32,
                                         c.c_void_p, c.c_char_p, c.c_int64, c.c_void_p,
                                         c.POINTER(c.c_double)]
@@ -61,7 +66,8 @@ def _declare(L):
     L.ccdgpu_last_stats.argtypes = [c.c_void_p, c.POINTER(abi.Stats)]
     L.ccdgpu_diag_counters.argtypes = [c.c_void_p, c.POINTER(c.c_uint64), c.c_int32]
     for name in ('ccdgpu_init', 'ccdgpu_destroy', 'ccdgpu_device_count', 'ccdgpu_synchronize',
-                 'ccdgpu_detect_batch', 'ccdgpu_stage', 'ccdgpu_stage_chipmunk', 'ccdgpu_staged_inputs',
+                 'ccdgpu_detect_batch', 'ccdgpu_stage', 'ccdgpu_stage_chips', 'ccdgpu_stage_slot_chips',
+                 'ccdgpu_fetch_batch_rows', 'ccdgpu_stage_chipmunk', 'ccdgpu_staged_inputs',
                  'ccdgpu_run_staged', 'ccdgpu_fetch_staged', 'ccdgpu_fetch_rows', 'ccdgpu_host_alloc',
                  'ccdgpu_host_free', 'ccdgpu_stage_slot', 'ccdgpu_run_slot', 'ccdgpu_rows_free', 'ccdgpu_fetch_rows',
                  'ccdgpu_last_stats', 'ccdgpu_diag_counters'):
@@ -74,7 +80,8 @@ EXPORTS = ('ccdgpu_version', 'ccdgpu_last_error', 'ccdgpu_params_default', 'ccdg
            'ccdgpu_result_free', 'ccdgpu_stage', 'ccdgpu_stage_chipmunk', 'ccdgpu_staged_inputs',
            'ccdgpu_run_staged', 'ccdgpu_fetch_staged', 'ccdgpu_fetch_rows', 'ccdgpu_rows_free',
            'ccdgpu_host_alloc', 'ccdgpu_host_free', 'ccdgpu_stage_slot', 'ccdgpu_run_slot',
-           'ccdgpu_last_stats', 'ccdgpu_diag_counters')
+           'ccdgpu_last_stats', 'ccdgpu_diag_counters', 'ccdgpu_stage_chips', 'ccdgpu_stage_slot_chips',
+           'ccdgpu_fetch_batch_rows')
 
 
 def lib():
@@ -113,6 +120,66 @@ def default_params():
     p = abi.Params()
     lib().ccdgpu_params_default(ctypes.byref(p))
     return p
+
+
+class ChipBatch(object):
+    """Host buffers of one staged batch in the ccdgpu_stage_chips layout (include/ccdgpu.h):
+    chips of their own pixel / observation counts packed back to back.  ``pinned=True``
+    allocates them in page-locked memory (ccdgpu_host_alloc) so uploads overlap detection.
+
+        b = ChipBatch([10000, 10000], [1421, 2121], pinned=True)
+        d, s, q = b.chip(1)      # views: dates [n], spectra [7][n_pix][n], qa [n_pix][n]
+    """
+
+    def __init__(self, n_pix, n_obs, pinned=False):
+        self.n_pix = np.ascontiguousarray(n_pix, dtype=np.int32).reshape(-1)
+        self.n_obs = np.ascontiguousarray(n_obs, dtype=np.int32).reshape(-1)
+        if self.n_pix.shape != self.n_obs.shape or self.n_pix.size == 0:
+            raise ValueError('n_pix and n_obs must be equal-length, non-empty')
+        self.obs_off = np.concatenate([[0], np.cumsum(self.n_obs, dtype=np.int64)])
+        self.pix_off = np.concatenate([[0], np.cumsum(self.n_pix, dtype=np.int64)])
+        self.data_off = np.concatenate([[0], np.cumsum(self.n_pix.astype(np.int64) * self.n_obs)])
+        alloc = pinned_empty if pinned else np.empty
+        self.dates = alloc((int(self.obs_off[-1]),), np.int64)
+        self.spectra = alloc((7 * int(self.data_off[-1]),), np.int16)
+        self.qa = alloc((int(self.data_off[-1]),), np.uint16)
+
+    @property
+    def n_chips(self):
+        return int(self.n_pix.size)
+
+    @property
+    def total_pixels(self):
+        return int(self.pix_off[-1])
+
+    @property
+    def nbytes(self):
+        return self.dates.nbytes + self.spectra.nbytes + self.qa.nbytes
+
+    def chip(self, c):
+        """Views of chip c: (dates [n], spectra [7][n_pix][n], qa [n_pix][n])."""
+        npx, n = int(self.n_pix[c]), int(self.n_obs[c])
+        o, d = int(self.obs_off[c]), int(self.data_off[c])
+        return (self.dates[o:o + n], self.spectra[7 * d:7 * (d + npx * n)].reshape(7, npx, n),
+                self.qa[d:d + npx * n].reshape(npx, n))
+
+    def set_chip(self, c, dates, spectra, qa):
+        d, s, q = self.chip(c)
+        d[...], s[...], q[...] = dates, spectra, qa
+
+    @classmethod
+    def from_chips(cls, chips, pinned=False):
+        """[(dates [n], spectra [7][n_pix][n], qa [n_pix][n]), ...] -> ChipBatch."""
+        chips = list(chips)
+        b = cls([c[2].shape[0] for c in chips], [c[0].shape[0] for c in chips], pinned=pinned)
+        for i, (d, s, q) in enumerate(chips):
+            b.set_chip(i, d, s, q)
+        return b
+
+    def mask_of(self, mask, c):
+        """Chip c's [n_pix][n_obs] block of a batch row fetch's flat mask."""
+        npx, n, d = int(self.n_pix[c]), int(self.n_obs[c]), int(self.data_off[c])
+        return mask[d:d + npx * n].reshape(npx, n)
 
 
 def _as_inputs(dates, spectra, qa):
@@ -178,6 +245,51 @@ class Context(object):
         self._keep = (dates, spectra, qa)
         self._n_pix = n_pix
 
+    def stage_chips(self, batch, params=None):
+        """Stage a ChipBatch (or a list of (dates, spectra, qa) chips of any sizes) in one
+        batch: ccdgpu_stage_chips."""
+        if not isinstance(batch, ChipBatch):
+            batch = ChipBatch.from_chips(batch)
+        p = params if isinstance(params, abi.Params) else abi.params_from_dict(params)
+        _check(lib().ccdgpu_stage_chips(self._ctx, ctypes.byref(p), batch.n_chips, batch.n_pix.ctypes.data,
+                                        batch.n_obs.ctypes.data, batch.dates.ctypes.data,
+                                        batch.spectra.ctypes.data, batch.qa.ctypes.data))
+        self._keep = batch
+        self._n_pix = None
+        return batch
+
+    def stage_slot_chips(self, slot, batch, params=None):
+        """Upload a ChipBatch into input slot 0/1 on the copy stream and return at once (the
+        batch must stay alive and unchanged until run_slot(slot) returns; pinned=True batches
+        upload asynchronously)."""
+        p = params if isinstance(params, abi.Params) else abi.params_from_dict(params)
+        _check(lib().ccdgpu_stage_slot_chips(self._ctx, int(slot), ctypes.byref(p), batch.n_chips,
+                                             batch.n_pix.ctypes.data, batch.n_obs.ctypes.data,
+                                             batch.dates.ctypes.data, batch.spectra.ctypes.data,
+                                             batch.qa.ctypes.data))
+        if not hasattr(self, '_slot_keep'):
+            self._slot_keep = {}
+        self._slot_keep[int(slot)] = batch
+
+    def fetch_batch_rows(self, cx, cy, width=100):
+        """Rows of every chip of the last run in one device pass and one copy: (row_offsets
+        [total_pixels+1], rows abi.ROW_DTYPE, mask int8 flat in the ChipBatch data layout --
+        ChipBatch.mask_of(mask, c) is chip c's [n_pix][n_obs] block)."""
+        batch = self._keep
+        if not isinstance(batch, ChipBatch):
+            raise ValueError('fetch_batch_rows needs a stage_chips / stage_slot_chips batch')
+        cx = np.ascontiguousarray(cx, dtype=np.int32)
+        cy = np.ascontiguousarray(cy, dtype=np.int32)
+        if cx.shape != (batch.n_chips,) or cy.shape != (batch.n_chips,):
+            raise ValueError('cx / cy need one entry per chip (%d)' % batch.n_chips)
+        r = abi.Rows()
+        rc = lib().ccdgpu_fetch_batch_rows(self._ctx, cx.ctypes.data, cy.ctypes.data, int(width), ctypes.byref(r))
+        try:
+            _check(rc)
+            return abi.unpack_rows(r, mask_len=int(batch.data_off[-1]))
+        finally:
+            lib().ccdgpu_rows_free(ctypes.byref(r))
+
     def stage_slot(self, slot, dates, spectra, qa, params=None):
         """Upload a batch into input slot 0/1 on the copy stream and return at once (the arrays
         must stay alive and unchanged until run_slot(slot) returns; pinned arrays from
@@ -199,7 +311,7 @@ class Context(object):
         if rc not in (0, abi.E_QA):
             _check(rc)
         self._keep = self._slot_keep.get(int(slot))
-        self._n_pix = self._keep[2].shape[1]
+        self._n_pix = None if isinstance(self._keep, ChipBatch) else self._keep[2].shape[1]
         return secs.value
 
     def stage_chipmunk(self, dates, text, offsets, n_pix, params=None):
@@ -227,7 +339,13 @@ class Context(object):
         return secs.value
 
     def staged_inputs(self):
-        """The staged pixel inputs copied back: (spectra [C][7][n_pix][n], qa [C][n_pix][n])."""
+        """The staged pixel inputs copied back: (spectra [C][7][n_pix][n], qa [C][n_pix][n]) for
+        a uniform batch, flat (spectra, qa) in the ChipBatch layout for a stage_chips batch."""
+        if isinstance(self._keep, ChipBatch):
+            b = self._keep
+            spectra, qa = np.empty_like(np.asarray(b.spectra)), np.empty_like(np.asarray(b.qa))
+            _check(lib().ccdgpu_staged_inputs(self._ctx, spectra.ctypes.data, qa.ctypes.data))
+            return spectra, qa
         d = self._keep[0]
         n_chips, n_obs = d.shape if d.ndim == 2 else (1, d.shape[0])
         n_pix = self._n_pix

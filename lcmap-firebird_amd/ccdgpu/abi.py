@@ -10,7 +10,7 @@ import numpy as np
 
 NBANDS = 7
 MAX_OBS = 4096
-MAX_PEEK = 64
+MAX_PEEK = 96
 BANDS = ('blue', 'green', 'red', 'nir', 'swir1', 'swir2', 'thermal')
 PROCEDURES = ('standard_procedure', 'permanent_snow_procedure', 'insufficient_clear_procedure')
 
@@ -84,13 +84,15 @@ class Rows(ctypes.Structure):
     ]
 
 
-def unpack_rows(r):
-    """ccdgpu_rows -> (row_offsets [n_pix+1], rows ROW_DTYPE [n_rows], mask int8 [n_pix][n_obs]),
-    copied out of library memory."""
+def unpack_rows(r, mask_len=None):
+    """ccdgpu_rows -> (row_offsets [n_pix+1], rows ROW_DTYPE [n_rows], mask int8 [n_pix][n_obs]
+    -- or, with mask_len, the flat mask of a batch fetch), copied out of library memory."""
     n_pix, n_obs, n = r.n_pix, r.n_obs, r.n_rows
     off = np.ctypeslib.as_array(r.row_offsets, shape=(n_pix + 1,)).copy()
     rows = np.frombuffer(ctypes.string_at(ctypes.cast(r.rows, ctypes.c_void_p), n * ROW_DTYPE.itemsize),
                          dtype=ROW_DTYPE).copy() if n else np.zeros(0, ROW_DTYPE)
+    if mask_len is not None:
+        return off, rows, np.ctypeslib.as_array(r.mask, shape=(max(int(mask_len), 1),))[:int(mask_len)].copy()
     mask = np.ctypeslib.as_array(r.mask, shape=(n_pix, n_obs)).copy()
     return off, rows, mask
 

@@ -56,12 +56,23 @@ def dates(cfg, chip):
     return out
 
 
-def chip(cfg, chip_index, pix0=0, n_pix=10000, chip_dates=None):
-    """Returns (dates[n] descending int64, spectra[7][n_pix][n] int16, qa[n_pix][n] uint16)."""
+def chip(cfg, chip_index, pix0=0, n_pix=10000, chip_dates=None, out=None):
+    """Returns (dates[n] descending int64, spectra[7][n_pix][n] int16, qa[n_pix][n] uint16).
+    out=(dates, spectra, qa): C-contiguous arrays of those shapes to fill in place (e.g. the
+    views of ccdgpu.ChipBatch.chip)."""
     d = dates(cfg, chip_index) if chip_dates is None else np.ascontiguousarray(chip_dates, dtype=np.int64)
     n = d.shape[0]
-    spectra = np.empty((7, n_pix, n), dtype=np.int16)
-    qa = np.empty((n_pix, n), dtype=np.uint16)
+    if out is not None:
+        od, spectra, qa = out
+        if (od.shape != (n,) or spectra.shape != (7, n_pix, n) or qa.shape != (n_pix, n) or
+                not (od.flags.c_contiguous and spectra.flags.c_contiguous and qa.flags.c_contiguous) or
+                od.dtype != np.int64 or spectra.dtype != np.int16 or qa.dtype != np.uint16):
+            raise ValueError('out arrays do not match chip %d (n_obs %d, n_pix %d)' % (chip_index, n, n_pix))
+        od[...] = d
+        d = od
+    else:
+        spectra = np.empty((7, n_pix, n), dtype=np.int16)
+        qa = np.empty((n_pix, n), dtype=np.uint16)
     lib().ccdsynth_chip(ctypes.byref(cfg), int(chip_index), int(pix0), int(n_pix), int(n),
                         d.ctypes.data, spectra.ctypes.data, qa.ctypes.data)
     return d, spectra, qa

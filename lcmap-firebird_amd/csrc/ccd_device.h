@@ -1,17 +1,22 @@
 // ccd_device.h -- device-side data contract shared by the HIP kernels and the host API.
 //
-// Layout in HBM (one "staged batch" = n_chips chips of n_pix pixels x n_obs observations):
-//   dates     int64 [n_chips][n_obs]            input order (merlin: descending)
-//   spectra   int16 [n_chips][7][n_pix][n_obs]  band-major, observation-contiguous (ABI layout)
-//   qa        uint16[n_chips][n_pix][n_obs]
-//   order     int32 [n_chips][n_obs]            sorted position -> input position (stable)
-//   sdates    int64 [n_chips][n_obs]            sorted dates
-//   basis     f64   [n_chips][n_obs][8]         t, cos wt, sin wt, cos 2wt, sin 2wt, cos 3wt, sin 3wt, 0
-//                                               (models/lasso.coefficient_matrix rows, shared by
-//                                                all 10^4 pixels of a chip)
-//   per wave slot scratch (persistent grid): compacted period of the current pixel
-//     cdate int32[n_obs], row {int16 v[7]; uint16 cidx}[n_obs]  (20 B / observation)
-//   outputs: mask bits, procedure, probs, per-pixel segment count, segment pool (+ seq numbers)
+// Layout in HBM.  One "staged batch" = n_chips chips (pixel groups sharing one date vector);
+// chip c has np_c = chip_npix[c] pixels and n_c = chip_nobs[c] observations, and its arrays are
+// packed back to back (a tile's base-cadence and sidelap chips stage together):
+//   dates     int64 [n_c]            at chip_obs_off[c]       input order (merlin: descending)
+//   spectra   int16 [7][np_c][n_c]   at 7 * chip_data_off[c]  band-major, observation-contiguous
+//   qa        uint16[np_c][n_c]      at chip_data_off[c]
+//   order     int32 [n_c]            at chip_obs_off[c]       sorted position -> input position
+//   sdates    int64 [n_c]            at chip_obs_off[c]       sorted dates
+//   basis     f64   [n_c][8]         at 8 * chip_obs_off[c]   t, cos wt, sin wt, cos 2wt, sin 2wt,
+//                                    cos 3wt, sin 3wt, 0 (models/lasso.coefficient_matrix rows,
+//                                    shared by all pixels of the chip)
+//   chip_obs_off = prefix sum of n_c, chip_pix_off = prefix sum of np_c (pixel p of the batch is
+//   pixel p - chip_pix_off[c] of chip c), chip_data_off = prefix sum of np_c * n_c.
+//   per wave slot scratch (persistent grid, sized by the largest n_c): compacted period of the
+//     current pixel, cdate int32[n], row {int16 v[7]; uint16 cidx}[n]  (20 B / observation)
+//   outputs: mask bits ([pixel][mask_words], mask_words from the largest n_c), procedure, probs,
+//   per-pixel segment count, segment pool (+ seq numbers)
 #pragma once
 #include <stdint.h>
 
@@ -27,11 +32,16 @@
 
 struct CcdDetectArgs {
     ccdgpu_params p;
-    int32_t n_chips, n_pix, n_obs, mask_words;
+    int32_t n_chips, n_obs_max, mask_words;
     int32_t n_slots;
+    int32_t poison;  // 1: every pixel starts from an LDS block filled with NaN bytes (test mode)
     int32_t pad0;
     int64_t total_pix;
     int64_t pool_cap;
+    const int32_t *chip_nobs;      // [n_chips]
+    const int64_t *chip_obs_off;   // [n_chips + 1]
+    const int64_t *chip_pix_off;   // [n_chips + 1]
+    const int64_t *chip_data_off;  // [n_chips + 1]
     const int16_t *spectra;
     const uint16_t *qa;
     const int32_t *order;
@@ -39,7 +49,8 @@ struct CcdDetectArgs {
     const double *basis;
     // work queue + global flags: [0] next pixel, [1] pool count, [2] first QA-error pixel (min),
     // [3] pool overflow, [4] first source line whose index guard tripped (0 = none),
-    // [5] / [6] s_memrealtime of the first wave's start / the last wave's end (100 MHz)
+    // [5] / [6] s_memrealtime of the first wave's start / the last wave's end (100 MHz),
+    // [7] first pixel whose adaptive peek exceeds CCDGPU_MAX_PEEK (min; ~0 = none)
     unsigned long long *counters;
     // per-slot scratch
     int32_t *s_date;
@@ -63,12 +74,12 @@ struct CcdDetectArgs {
 extern "C" {
 #endif
 // kernel launchers (ccd_kernels.hip)
-int ccdk_prep(const int64_t *dates, int32_t n_chips, int32_t n_obs, double avg_days_yr,
-              int32_t *order, int64_t *sdates, double *basis, void *stream);
+int ccdk_prep(const int64_t *dates, int32_t n_chips, const int32_t *chip_nobs, const int64_t *chip_obs_off,
+              double avg_days_yr, int32_t *order, int64_t *sdates, double *basis, void *stream);
 // the detection kernel reads its arguments from slot arg_slot of a __constant__ array (one slot
 // per live context, so contexts on one device may launch concurrently from their own streams)
 int ccdk_set_args(const CcdDetectArgs *host_args, int arg_slot, void *stream);
-int ccdk_detect(int32_t grid, int variant, int32_t n_obs, int arg_slot, void *stream);
+int ccdk_detect(int32_t grid, int variant, int32_t n_obs_max, int arg_slot, void *stream);
 // 1 if this build keeps the compacted period in LDS (-DCCD_PERIOD_IN_LDS)
 int ccdk_period_in_lds(void);
 // dynamic LDS bytes per wave and resident waves per CU for a period of n_obs observations
@@ -82,8 +93,10 @@ int ccdk_unpack_b64(const unsigned char *text, int64_t text_bytes, const int64_t
 int ccdk_pack_rows(const ccdgpu_segment *seg, const int64_t *seg_off, const int64_t *row_off, const uint32_t *mask_bits,
                    int32_t mask_words, int32_t n_pix, int32_t n_obs, int32_t cx, int32_t cy, int32_t width,
                    ccdgpu_row *rows, int8_t *mask, void *stream);
+// pool -> CSR; the segment's pixel field becomes the pixel index within its chip
 int ccdk_scatter(const ccdgpu_segment *pool, const int32_t *pool_seq, int64_t n_pool,
-                 const int64_t *offsets, int32_t n_pix_per_chip, ccdgpu_segment *out, void *stream);
+                 const int64_t *offsets, const int64_t *chip_pix_off, int32_t n_chips, ccdgpu_segment *out,
+                 void *stream);
 #ifdef __cplusplus
 }
 #endif

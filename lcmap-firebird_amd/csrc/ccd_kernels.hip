@@ -39,9 +39,10 @@ constexpr int W = CCD_WAVE;
 constexpr int RW = 16;  // doubles per staged design row: t c1 s1 c2 s2 c3 s3 _ y0..y6 _
 constexpr int TR = 32;  // rows per LDS staging tile
 constexpr int MAXW = CCDGPU_MAX_OBS / 32;
+constexpr int PSTR = CCDGPU_MAX_PEEK;  // band stride of the peek-residual ring
 #define CCD_NPHASE (CCD_NSTATS - 8)
 
-static_assert(TR * RW >= CCDGPU_MAX_PEEK * 8, "row buffer holds the peek residuals");
+static_assert(PSTR >= CCD_WAVE, "the ring holds a lookforward batch's 64 rows per band");
 // Global-memory pointers kept in the per-pixel state are typed address_space(1) so every access
 // is a global_* instruction (a generic pointer would compile to flat_*, which also counts against
 // lgkmcnt and makes every later LDS wait wait for the global load too).
@@ -50,7 +51,10 @@ template <class T>
 __device__ __forceinline__ GLOBAL_AS T *as_global(T *p) { return (GLOBAL_AS T *)p; }
 
 struct __attribute__((aligned(16))) Lds {
-    double row[TR][RW];  // staging tile; also holds the last peek residuals (64 obs x 8 bands)
+    union {
+        double row[TR][RW];       // staging tile (Gram, Tmask, speculative fits, variogram counts)
+        double ring[NB * PSTR];   // peek residuals, band-major [band][PSTR] (never live with a tile)
+    };
     double G[8][8];
     double Q[8][8];  // Q[j][band] = Xc_j . yc_band
     double YY[8];
@@ -93,11 +97,10 @@ __device__ __forceinline__ const CcdDetectArgs &ARGS() {
 }
 extern __shared__ __attribute__((aligned(16))) char ccd_smem[];
 __device__ __forceinline__ Lds &LDS() { return *reinterpret_cast<Lds *>(ccd_smem); }
-// Peek-residual ring, band-major [band][64 observations], in the row staging tile (the Gram
-// staging never overlaps a live ring): lane-contiguous, so lane-per-observation access is
-// bank-conflict free.
-__device__ __forceinline__ double *PRES(Lds *L) { return &L->row[0][0]; }
-static_assert(TR * RW >= 8 * CCD_WAVE, "row tile holds the 8 x 64 residual ring");
+// Peek-residual ring, band-major [band][PSTR observations], aliased with the row staging tile
+// (the Gram staging never overlaps a live ring): lane-contiguous, so lane-per-observation access
+// is bank-conflict free.
+__device__ __forceinline__ double *PRES(Lds *L) { return &L->ring[0]; }
 
 // One compacted observation: the 7 band values and its sorted-date index in one 16-byte row, so a
 // random gather (closest-DOY, peek) touches one cache line instead of eight.
@@ -1035,6 +1038,11 @@ __device__ __forceinline__ void adjust_peek(Px &P) {
     const double delta = narrow ? median_u16(gen, P.m - 1, P.m - 1, true) : median_int(gen, P.m - 1, P.m - 1, 0, 1 << 30);
     const double adj = rint((double)(p.peek_size * 16) / delta);
     if (adj > (double)p.peek_size) {
+        // With the default PEEK_SIZE (6) the peek is at most 96 = CCDGPU_MAX_PEEK: the compacted
+        // period has distinct dates, so the median gap is >= 1 day.  A larger configured
+        // PEEK_SIZE can exceed it: the pixel is reported (the call fails with CCDGPU_EOVERFLOW)
+        // and finished with the largest supported peek so the launch still drains.
+        if (adj > (double)CCDGPU_MAX_PEEK && lane() == 0) atomicMin(&ARGS().counters[7], (unsigned long long)P.gpix);
         P.peek = adj > (double)CCDGPU_MAX_PEEK ? CCDGPU_MAX_PEEK : (int)adj;
         P.chg = ARGS().thr_table[P.peek];
     }
@@ -1632,14 +1640,14 @@ __device__ __forceinline__ bool eval_peek(Px &P, int k, int start, int dir, doub
         rr[pass] = (pass * 8 < k && jj < k && bnd < NB) ? resid_at(P, bnd, start + dir * jj) : 0.0;
     }
 #pragma unroll
-    for (int pass = 0; pass < 8; ++pass) {
+    for (int pass = 0; pass < PSTR / 8; ++pass) {
         if (pass * 8 >= k) break;
         const int jj = pass * 8 + osub;
         const bool valid = jj < k && bnd < NB;
         double r = 0.0;
         if (pass < 4) r = rr[pass < 4 ? pass : 0];
         else if (valid) r = resid_at(P, bnd, start + dir * jj);
-        if (jj < k && bnd < NB) PRES(L)[bnd * W + jj] = r;  // kept for the segment's magnitude medians
+        if (jj < k && bnd < NB) PRES(L)[bnd * PSTR + jj] = r;  // kept for the segment's magnitude medians
         const double v = r / rm;
         const double mag = gsum8((valid && det) ? v * v : 0.0);
         if (bal(bnd == 0 && jj < k && !(mag > P.chg))) all = false;
@@ -1659,7 +1667,7 @@ __device__ __forceinline__ double peek_medians(Px &P, int k, int off) {
     const int l = lane();
     const int bnd = l & 7, osub = l >> 3;
     const int t1 = (k - 1) / 2, t2 = k / 2;
-    const double *R = PRES(L) + bnd * W + off;
+    const double *R = PRES(L) + bnd * PSTR + off;
     for (int jj = osub; jj < k; jj += 8) {
         if (bnd >= NB) continue;
         const double v = R[jj];
@@ -1947,7 +1955,7 @@ __device__ __forceinline__ void ring_rows(const Px &P, int x0) {
 #pragma unroll
             for (int jj = 1; jj < 7; ++jj) pr += x[jj] * c[jj];
             pr += c[7];
-            R[bd * W] = (double)cw.v[bd] - pr;
+            R[bd * PSTR] = (double)cw.v[bd] - pr;
         }
     }
     wsync();
@@ -2383,6 +2391,41 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
             b += 1;
             continue;
         }
+        if (k > W) {
+            // A peek longer than the 64-row ring (adaptive peek > 64: median date gap < 1.5
+            // days) runs one step at a time in change.lookforward's own order: refit on the span
+            // test, comparison rmse from the 24 closest-DOY fit observations of the peek end.
+            nc = num_coefs(p, b - a);
+            peek_start = b;
+            const double span = (double)CDR(P, b - 1) - (double)CDR(P, a);
+            if (span >= 1.33 * fit_span) {
+                fa = a;
+                fb = b;
+                fit_span = span;
+                fit_models(P, fa, fb, nc, fb - fa <= 24);
+                nc_fit = nc;
+            }
+            if (fb - fa > 24 && (hfa != fa || hfb != fb)) {
+                build_closest(P, fa, fb, nc_fit);
+                hfa = fa;
+                hfb = fb;
+            }
+            closest_doy_scan(P, fa, fb, b + k - 1);
+            double m0;
+            const bool chg_now = eval_peek(P, k, b, 1, m0);
+            moff = 0;
+            if (chg_now) {
+                change = 1.0;
+                break;
+            }
+            if (m0 > p.outlier_threshold) {
+                const int rm = b;
+                compact_drop(P, rm, [&](int j) { return j == rm; });
+                continue;
+            }
+            b += 1;
+            continue;
+        }
         // ---- batch of up to B steps at window starts x0 .. x0 + B - 1 (model fixed)
         const int nf = fb - fa;
         if (nf > 24 && (hfa != fa || hfb != fb)) {
@@ -2450,7 +2493,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
 #pragma unroll
-                    for (int t = 0; t < NB; ++t) rv[u][t] = t < nd ? R[bs[t] * W + j0 + u] : 0.0;
+                    for (int t = 0; t < NB; ++t) rv[u][t] = t < nd ? R[bs[t] * PSTR + j0 + u] : 0.0;
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
@@ -2562,10 +2605,11 @@ __device__ __forceinline__ int px_setup(Px &P, int chip, int pix) {
     Lds *L = &LDS();
     const int l = lane();
     const int n = P.n;
-    const int32_t *order = A.order + (size_t)chip * n;
-    const uint16_t *qa = A.qa + ((size_t)chip * A.n_pix + pix) * n;
-    const size_t bstride = (size_t)A.n_pix * n;
-    const int16_t *sp = A.spectra + (size_t)chip * NB * bstride + (size_t)pix * n;
+    const int64_t data_off = A.chip_data_off[chip];
+    const int32_t *order = A.order + A.chip_obs_off[chip];
+    const uint16_t *qa = A.qa + data_off + (size_t)pix * n;
+    const size_t bstride = (size_t)(A.chip_pix_off[chip + 1] - A.chip_pix_off[chip]) * n;
+    const int16_t *sp = A.spectra + (size_t)NB * data_off + (size_t)pix * n;
     int c_clear = 0, c_water = 0, c_snow = 0, c_cloud = 0, c_fill = 0;
     bool bad = false;
     // (four 64-observation chunks per round, their dependent order -> qa loads issued together;
@@ -2704,14 +2748,14 @@ __device__ __forceinline__ void detect_body() {
     Lds &lds = LDS();
     const int l = lane();
     const int slot = blockIdx.x;
+    const size_t nmax = (size_t)A.n_obs_max;  // per-slot scratch stride
     Px P;
-    P.n = A.n_obs;
 #ifndef CCD_PERIOD_IN_LDS
-    P.cd = A.s_date + (size_t)slot * A.n_obs;
-    P.cr = reinterpret_cast<CRow *>(A.s_row) + (size_t)slot * A.n_obs;
+    P.cd = A.s_date + (size_t)slot * nmax;
+    P.cr = reinterpret_cast<CRow *>(A.s_row) + (size_t)slot * nmax;
 #endif
-    P.fs = as_global(A.s_f64 + (size_t)slot * 8 * A.n_obs);
-    P.bk = as_global(A.s_bk + (size_t)slot * A.n_obs);
+    P.fs = as_global(A.s_f64 + (size_t)slot * 8 * nmax);
+    P.bk = as_global(A.s_bk + (size_t)slot * nmax);
     P.fits = 0;
     P.sweeps = 0;
     P.bad = 0;
@@ -2728,15 +2772,41 @@ __device__ __forceinline__ void detect_body() {
         if (l == 0) job = atomicAdd(&A.counters[0], 1ull);
         job = __shfl((unsigned long long)job, 0);
         if (job >= (unsigned long long)A.total_pix) break;
-        const int chip = (int)(job / (unsigned long long)A.n_pix);
-        const int pix = (int)(job % (unsigned long long)A.n_pix);
+        // chip of this pixel: binary search of the chips' pixel offsets (wave-uniform)
+        int lo = 0, hi = A.n_chips - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if ((unsigned long long)A.chip_pix_off[mid] <= job) lo = mid;
+            else hi = mid - 1;
+        }
+        const int chip = lo;
+        const int pix = (int)(job - (unsigned long long)A.chip_pix_off[chip]);
+        const int64_t obs_off = A.chip_obs_off[chip];
+        P.n = A.chip_nobs[chip];
         P.gpix = (int64_t)job;
         P.nseg = 0;
         P.acc_a = -1;
         P.acc_b = 0;
         P.fit_k = 0;
-        P.basis = as_global(A.basis + (size_t)chip * A.n_obs * CCD_BASIS_STRIDE);
-        P.sd = A.sdates + (size_t)chip * A.n_obs;
+        P.basis = as_global(A.basis + (size_t)obs_off * CCD_BASIS_STRIDE);
+        P.sd = A.sdates + obs_off;
+#ifndef CCD_PHASE_TIMERS
+        if (A.poison) {
+            // test mode: no value may come from a previous pixel's (or wave's) LDS contents
+            uint4 *w = reinterpret_cast<uint4 *>(&lds);
+            for (int i = l; i < (int)(sizeof(Lds) / 16); i += W) w[i] = uint4{~0u, ~0u, ~0u, ~0u};
+            // ... nor from the slot's global scratch
+            for (size_t i = l; i < 8 * nmax; i += W) P.fs[i] = __longlong_as_double(-1ll);
+            for (size_t i = l; i < nmax; i += W) P.bk[i] = 0xFFFFu;
+#ifndef CCD_PERIOD_IN_LDS
+            for (size_t i = l; i < nmax; i += W) {
+                P.cd[i] = -1;
+                reinterpret_cast<uint4 *>(P.cr)[i] = uint4{~0u, ~0u, ~0u, ~0u};
+            }
+#endif
+            gsync();
+        }
+#endif
         PH_BEGIN(tot)
         PH_BEGIN(su)
         const int proc = px_setup(P, chip, pix);
@@ -2754,7 +2824,7 @@ __device__ __forceinline__ void detect_body() {
             standard_procedure(P);
         } else if (P.m >= A.p.meow_size) {
             fit_models(P, 0, P.m, A.p.coef_min);
-            emit(P, (int)P.sd[0], (int)P.sd[A.n_obs - 1], 0, P.m, 0.0,
+            emit(P, (int)P.sd[0], (int)P.sd[P.n - 1], 0, P.m, 0.0,
                  proc == CCDGPU_PROC_PERMANENT_SNOW ? A.p.curve_qa_persist_snow : A.p.curve_qa_insuf_clear, 0.0);
         }
         wsync();
@@ -2805,13 +2875,16 @@ __global__ __launch_bounds__(64, 4) __attribute__((flatten)) void ccd_detect_w4(
 // One 256-thread block per chip: stable rank of each date (ties by input position), sorted
 // dates, order, and the coefficient_matrix rows (w = 2 pi / avg_days_yr; cos/sin of w t, 2 w t,
 // 3 w t exactly as models/lasso.coefficient_matrix forms them).
-__global__ __launch_bounds__(256) void ccd_prep(const int64_t *dates, int n, double avg_days_yr,
+__global__ __launch_bounds__(256) void ccd_prep(const int64_t *dates, const int32_t *chip_nobs,
+                                                const int64_t *chip_obs_off, double avg_days_yr,
                                                 int32_t *order, int64_t *sdates, double *basis) {
     const int chip = blockIdx.x;
-    const int64_t *d = dates + (size_t)chip * n;
-    int32_t *ord = order + (size_t)chip * n;
-    int64_t *sd = sdates + (size_t)chip * n;
-    double *bs = basis + (size_t)chip * n * CCD_BASIS_STRIDE;
+    const int n = chip_nobs[chip];
+    const int64_t off = chip_obs_off[chip];
+    const int64_t *d = dates + off;
+    int32_t *ord = order + off;
+    int64_t *sd = sdates + off;
+    double *bs = basis + (size_t)off * CCD_BASIS_STRIDE;
     __shared__ int64_t sdl[CCDGPU_MAX_OBS];
     for (int i = threadIdx.x; i < n; i += blockDim.x) sdl[i] = d[i];
     __syncthreads();
@@ -2842,26 +2915,32 @@ __global__ __launch_bounds__(256) void ccd_prep(const int64_t *dates, int n, dou
 
 // Pool -> CSR: one wave per pooled segment, dwords copied lane-parallel.
 __global__ __launch_bounds__(256) void ccd_scatter(const ccdgpu_segment *pool, const int32_t *seq, int64_t n_pool,
-                                                   const int64_t *offsets, int n_pix_per_chip,
-                                                   ccdgpu_segment *out) {
+                                                   const int64_t *offsets, const int64_t *chip_pix_off,
+                                                   int n_chips, ccdgpu_segment *out) {
     const int64_t s = (int64_t)blockIdx.x * (blockDim.x / W) + threadIdx.x / W;
     if (s >= n_pool) return;
     const int l = threadIdx.x % W;
     const int gp = pool[s].pixel;
+    int lo = 0, hi = n_chips - 1;  // chip of the pixel
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (chip_pix_off[mid] <= gp) lo = mid;
+        else hi = mid - 1;
+    }
     const int64_t dst = offsets[gp] + seq[s];
     const uint32_t *src = reinterpret_cast<const uint32_t *>(pool + s);
     uint32_t *dd = reinterpret_cast<uint32_t *>(out + dst);
     constexpr int NW = (int)(sizeof(ccdgpu_segment) / 4);
     constexpr int PIXW = (int)(offsetof(ccdgpu_segment, pixel) / 4);
-    for (int i = l; i < NW; i += W) dd[i] = (i == PIXW) ? (uint32_t)(gp % n_pix_per_chip) : src[i];
+    for (int i = l; i < NW; i += W) dd[i] = (i == PIXW) ? (uint32_t)(gp - chip_pix_off[lo]) : src[i];
 }
 
 }  // namespace
 
-extern "C" int ccdk_prep(const int64_t *dates, int32_t n_chips, int32_t n_obs, double avg_days_yr,
-                         int32_t *order, int64_t *sdates, double *basis, void *stream) {
-    hipLaunchKernelGGL(ccd_prep, dim3(n_chips), dim3(256), 0, (hipStream_t)stream, dates, n_obs,
-                       avg_days_yr, order, sdates, basis);
+extern "C" int ccdk_prep(const int64_t *dates, int32_t n_chips, const int32_t *chip_nobs, const int64_t *chip_obs_off,
+                         double avg_days_yr, int32_t *order, int64_t *sdates, double *basis, void *stream) {
+    hipLaunchKernelGGL(ccd_prep, dim3(n_chips), dim3(256), 0, (hipStream_t)stream, dates, chip_nobs,
+                       chip_obs_off, avg_days_yr, order, sdates, basis);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2920,12 +2999,12 @@ extern "C" int ccdk_detect(int32_t grid, int variant, int32_t n_obs, int arg_slo
 }
 
 extern "C" int ccdk_scatter(const ccdgpu_segment *pool, const int32_t *pool_seq, int64_t n_pool,
-                            const int64_t *offsets, int32_t n_pix_per_chip, ccdgpu_segment *out,
-                            void *stream) {
+                            const int64_t *offsets, const int64_t *chip_pix_off, int32_t n_chips,
+                            ccdgpu_segment *out, void *stream) {
     if (n_pool <= 0) return 0;
     const int per_block = 256 / W;
     const int64_t blocks = (n_pool + per_block - 1) / per_block;
     hipLaunchKernelGGL(ccd_scatter, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, pool,
-                       pool_seq, n_pool, offsets, n_pix_per_chip, out);
+                       pool_seq, n_pool, offsets, chip_pix_off, n_chips, out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -1,9 +1,10 @@
 // ccdgpu_api.cpp -- host side of the C-ABI declared in include/ccdgpu.h.
 //
-// Owns device memory and one HIP stream per context.  A detection call = H2D of the chip stack
-// (band-major, observation-contiguous, exactly the layout the Python packer hands over), the
-// per-chip prep kernel, the persistent per-pixel detection kernel, an exclusive scan of the
-// per-pixel segment counts (hipCUB) and the pool->CSR scatter, then D2H of the CSR result.
+// Owns device memory and two HIP streams per context.  A detection call = H2D of the chip stacks
+// (band-major, observation-contiguous, exactly the layout the Python packer hands over; chips of
+// different observation counts packed back to back), the per-chip prep kernel, the persistent
+// per-pixel detection kernel, an exclusive scan of the per-pixel segment counts (hipCUB) and the
+// pool->CSR scatter, then D2H of the CSR result or of the device-packed table rows.
 // Replaces the per-pixel ccd.detect call of ccdc/pyccd.py:168 (see include/ccdgpu.h).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -94,6 +95,40 @@ void release_arg_slot(int i) {
     g_slots_used &= ~(1u << i);
 }
 
+// Shape of a staged batch: per-chip pixel / observation counts and their prefix sums
+// (ccd_device.h layout).
+struct Shape {
+    std::vector<int32_t> npix, nobs;
+    std::vector<int64_t> obs_off, pix_off, data_off;  // [n_chips + 1]
+    int32_t n_obs_max = 0;
+    int n_chips() const { return (int)npix.size(); }
+    int64_t total_obs() const { return obs_off.empty() ? 0 : obs_off.back(); }
+    int64_t total_pix() const { return pix_off.empty() ? 0 : pix_off.back(); }
+    int64_t total_data() const { return data_off.empty() ? 0 : data_off.back(); }
+};
+
+int make_shape(int32_t n_chips, const int32_t *n_pix, const int32_t *n_obs, Shape &s) {
+    if (n_chips <= 0) return fail(CCDGPU_EINVAL, "n_chips must be > 0");
+    if (!n_pix || !n_obs) return fail(CCDGPU_EINVAL, "NULL n_pix / n_obs array");
+    s.npix.assign(n_pix, n_pix + n_chips);
+    s.nobs.assign(n_obs, n_obs + n_chips);
+    s.obs_off.assign(n_chips + 1, 0);
+    s.pix_off.assign(n_chips + 1, 0);
+    s.data_off.assign(n_chips + 1, 0);
+    s.n_obs_max = 0;
+    for (int c = 0; c < n_chips; ++c) {
+        if (n_pix[c] <= 0) return fail(CCDGPU_EINVAL, "chip " + std::to_string(c) + ": n_pix must be > 0");
+        if (n_obs[c] <= 0 || n_obs[c] > CCDGPU_MAX_OBS)
+            return fail(CCDGPU_EINVAL, "chip " + std::to_string(c) + ": n_obs must be in [1, " + std::to_string(CCDGPU_MAX_OBS) + "]");
+        s.obs_off[c + 1] = s.obs_off[c] + n_obs[c];
+        s.pix_off[c + 1] = s.pix_off[c] + n_pix[c];
+        s.data_off[c + 1] = s.data_off[c] + (int64_t)n_pix[c] * n_obs[c];
+        s.n_obs_max = std::max(s.n_obs_max, n_obs[c]);
+    }
+    if (s.total_pix() >= (int64_t)1 << 31) return fail(CCDGPU_EINVAL, "more than 2^31 - 1 pixels in one batch");
+    return 0;
+}
+
 }  // namespace
 
 struct ccdgpu_ctx {
@@ -101,6 +136,7 @@ struct ccdgpu_ctx {
     int n_cu = 0;
     int slots_per_cu = 0;
     int variant = 3;  // detection kernel register budget: 1..4 waves/SIMD (CCDGPU_KERNEL=w1..w4)
+    int poison = 0;   // CCDGPU_POISON=1: LDS and slot scratch filled with NaN bytes per pixel (test mode)
     int arg_slot = -1;  // this context's launch-argument slot in constant memory
     hipStream_t stream = nullptr;
     hipStream_t copy_stream = nullptr;  // uploads of ccdgpu_stage_slot (overlap a running detection)
@@ -113,12 +149,14 @@ struct ccdgpu_ctx {
     // staged batch
     bool staged = false, ran = false;
     ccdgpu_params params{};
-    int32_t n_chips = 0, n_pix = 0, n_obs = 0, mask_words = 0, n_slots = 0;
+    Shape shape;
+    int32_t mask_words = 0, n_slots = 0;
     int64_t total_pix = 0, pool_cap = 0, n_pool = 0;
     DevBuf<int64_t> dates, sdates, offsets;
     DevBuf<int16_t> spectra;
     DevBuf<uint16_t> qa;
-    DevBuf<int32_t> order, procedure, nseg, pool_seq;
+    DevBuf<int32_t> order, procedure, nseg, pool_seq, chip_nobs;
+    DevBuf<int64_t> chip_obs_off, chip_pix_off, chip_data_off;
     DevBuf<double> basis, probs, s_f64;
     DevBuf<unsigned long long> counters, stats;
     DevBuf<int32_t> s_date;
@@ -126,15 +164,16 @@ struct ccdgpu_ctx {
     DevBuf<uint16_t> s_bk;
     DevBuf<uint32_t> mask;
     DevBuf<ccdgpu_segment> pool, csr;
-    DevBuf<CcdDetectArgs> args;
     DevBuf<unsigned char> cub_tmp;
-    DevBuf<ccdgpu_row> rows;    // output writer scratch (ccdgpu_fetch_rows)
+    DevBuf<ccdgpu_row> rows;    // output writer scratch (ccdgpu_fetch_rows / ccdgpu_fetch_batch_rows)
     DevBuf<int64_t> row_off, seg_off1;
+    DevBuf<int32_t> row_xy;     // per-chip (cx, cy) of a batch row fetch
     DevBuf<int8_t> mask8;
     DevBuf<int64_t> slot_dates[2];   // double-buffered inputs (ccdgpu_stage_slot / ccdgpu_run_slot)
     DevBuf<int16_t> slot_spectra[2];
     DevBuf<uint16_t> slot_qa[2];
-    int32_t slot_shape[2][3] = {{0, 0, 0}, {0, 0, 0}};
+    Shape slot_shape[2];
+    ccdgpu_params slot_params[2];
     bool slot_ready[2] = {false, false};
     DevBuf<unsigned char> b64;  // chipmunk payload text of the last ccdgpu_stage_chipmunk
     DevBuf<int64_t> b64_off;
@@ -142,10 +181,11 @@ struct ccdgpu_ctx {
     ccdgpu_stats last{};
     unsigned long long diag[CCD_NSTATS] = {};
     ~ccdgpu_ctx() {
-        for (auto *b : {&dates, &sdates, &offsets}) b->release();
+        for (auto *b : {&dates, &sdates, &offsets, &chip_obs_off, &chip_pix_off, &chip_data_off, &row_off, &seg_off1, &b64_off})
+            b->release();
         spectra.release();
         qa.release();
-        for (auto *b : {&order, &procedure, &nseg, &pool_seq, &s_date}) b->release();
+        for (auto *b : {&order, &procedure, &nseg, &pool_seq, &s_date, &chip_nobs, &row_xy}) b->release();
         for (auto *b : {&basis, &probs, &s_f64}) b->release();
         counters.release();
         stats.release();
@@ -154,10 +194,8 @@ struct ccdgpu_ctx {
         mask.release();
         pool.release();
         csr.release();
-        args.release();
         cub_tmp.release();
         b64.release();
-        b64_off.release();
         for (int i = 0; i < 2; ++i) {
             slot_dates[i].release();
             slot_spectra[i].release();
@@ -166,8 +204,6 @@ struct ccdgpu_ctx {
         }
         if (copy_stream) (void)hipStreamDestroy(copy_stream);
         rows.release();
-        row_off.release();
-        seg_off1.release();
         mask8.release();
         for (auto &e : ev)
             if (e) (void)hipEventDestroy(e);
@@ -178,7 +214,7 @@ struct ccdgpu_ctx {
 
 extern "C" {
 
-const char *ccdgpu_version(void) { return "ccdgpu 0.1.0 (gfx950; lcmap-pyccd:2018.03.12.dev-ncompare.b2 semantics)"; }
+const char *ccdgpu_version(void) { return "ccdgpu 0.2.0 (gfx950; lcmap-pyccd:2018.03.12.dev-ncompare.b2 semantics)"; }
 
 const char *ccdgpu_last_error(void) { return g_err.c_str(); }
 
@@ -279,6 +315,7 @@ int ccdgpu_init(int device, ccdgpu_ctx **out) {
         if (v[0] == 'w' && v[1] >= '1' && v[1] <= '4' && v[2] == 0) c->variant = v[1] - '0';
     }
     if (const char *v = std::getenv("CCDGPU_SLOTS_PER_CU")) c->slots_per_cu = std::max(1, std::atoi(v));
+    if (const char *v = std::getenv("CCDGPU_POISON")) c->poison = std::atoi(v) != 0;
     *out = c;
     return 0;
 }
@@ -287,6 +324,7 @@ int ccdgpu_destroy(ccdgpu_ctx *ctx) {
     if (!ctx) return 0;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
+    (void)hipStreamSynchronize(ctx->copy_stream);
     delete ctx;
     return 0;
 }
@@ -298,11 +336,8 @@ int ccdgpu_synchronize(ccdgpu_ctx *ctx) {
     return 0;
 }
 
-static int check_params(const ccdgpu_params *p, int32_t n_pix, int32_t n_obs) {
+static int check_params(const ccdgpu_params *p) {
     if (!p) return fail(CCDGPU_EINVAL, "params is NULL");
-    if (n_pix <= 0) return fail(CCDGPU_EINVAL, "n_pix must be > 0");
-    if (n_obs <= 0 || n_obs > CCDGPU_MAX_OBS)
-        return fail(CCDGPU_EINVAL, "n_obs must be in [1, " + std::to_string(CCDGPU_MAX_OBS) + "]");
     if (p->peek_size < 1 || p->peek_size > CCDGPU_MAX_PEEK)
         return fail(CCDGPU_EINVAL, "peek_size must be in [1, " + std::to_string(CCDGPU_MAX_PEEK) + "]");
     if (p->meow_size < 5) return fail(CCDGPU_EINVAL, "meow_size must be >= 5 (Tmask needs > 4 observations)");
@@ -316,64 +351,82 @@ static int check_params(const ccdgpu_params *p, int32_t n_pix, int32_t n_obs) {
     return 0;
 }
 
-// Device buffers of a staged batch (inputs, per-slot scratch, outputs) and the dates upload;
-// the pixel data are filled by the caller (a plain upload or the chipmunk decoder).
-static int stage_alloc(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_chips, int32_t n_pix, int32_t n_obs,
-                       const int64_t *dates, bool base_inputs = true) {
+// Device buffers of a staged batch (chip tables, per-slot scratch, outputs) and, with
+// base_inputs, the input buffers plus the dates upload; the pixel data are filled by the caller
+// (a plain upload or the chipmunk decoder).
+static int stage_alloc(ccdgpu_ctx *c, const ccdgpu_params *params, const Shape &sh, const int64_t *dates,
+                       bool base_inputs = true) {
     if (!c) return fail(CCDGPU_EINVAL, "NULL ctx");
-    if (n_chips <= 0) return fail(CCDGPU_EINVAL, "n_chips must be > 0");
-    int rc = check_params(params, n_pix, n_obs);
+    int rc = check_params(params);
     if (rc) return rc;
     HIPCHK(hipSetDevice(c->device));
     c->staged = false;
     c->params = *params;
-    c->n_chips = n_chips;
-    c->n_pix = n_pix;
-    c->n_obs = n_obs;
-    c->mask_words = (n_obs + 31) / 32;
-    c->total_pix = (int64_t)n_chips * n_pix;
-    const size_t nc = (size_t)n_chips, np = (size_t)n_pix, no = (size_t)n_obs;
-    if (base_inputs && ((rc = c->dates.ensure(nc * no)) || (rc = c->spectra.ensure(nc * 7 * np * no)) ||
-                        (rc = c->qa.ensure(nc * np * no))))
+    c->shape = sh;
+    const int nc = sh.n_chips();
+    c->mask_words = (sh.n_obs_max + 31) / 32;
+    c->total_pix = sh.total_pix();
+    const size_t tobs = (size_t)sh.total_obs(), tdata = (size_t)sh.total_data();
+    if (base_inputs && ((rc = c->dates.ensure(tobs)) || (rc = c->spectra.ensure(7 * tdata)) || (rc = c->qa.ensure(tdata))))
         return rc;
-    if ((rc = c->order.ensure(nc * no)) ||
-        (rc = c->sdates.ensure(nc * no)) || (rc = c->basis.ensure(nc * no * CCD_BASIS_STRIDE)) ||
+    if ((rc = c->order.ensure(tobs)) || (rc = c->sdates.ensure(tobs)) || (rc = c->basis.ensure(tobs * CCD_BASIS_STRIDE)) ||
+        (rc = c->chip_nobs.ensure(nc)) || (rc = c->chip_obs_off.ensure(nc + 1)) || (rc = c->chip_pix_off.ensure(nc + 1)) ||
+        (rc = c->chip_data_off.ensure(nc + 1)) ||
         (rc = c->procedure.ensure(c->total_pix)) || (rc = c->nseg.ensure(c->total_pix)) ||
         (rc = c->probs.ensure(3 * c->total_pix)) || (rc = c->offsets.ensure(c->total_pix + 1)) ||
         (rc = c->mask.ensure((size_t)c->total_pix * c->mask_words)) || (rc = c->counters.ensure(8)) ||
-        (rc = c->stats.ensure(CCD_NSTATS)) || (rc = c->args.ensure(1)))
+        (rc = c->stats.ensure(CCD_NSTATS)))
         return rc;
     // persistent grid: one wave slot per resident wave (LDS / register occupancy), capped by
     // CCDGPU_SLOTS_PER_CU
-    const int occ = ccdk_occupancy(c->variant, n_obs);
-    if (occ <= 0) return fail(CCDGPU_EHIP, "detection kernel cannot be resident with " + std::to_string(ccdk_lds_bytes(n_obs)) + " B of LDS");
+    const int occ = ccdk_occupancy(c->variant, sh.n_obs_max);
+    if (occ <= 0) return fail(CCDGPU_EHIP, "detection kernel cannot be resident with " + std::to_string(ccdk_lds_bytes(sh.n_obs_max)) + " B of LDS");
     c->n_slots = (int32_t)std::min<int64_t>(c->total_pix, (int64_t)c->n_cu * std::min(occ, c->slots_per_cu));
-    const size_t ns = (size_t)c->n_slots;
+    const size_t ns = (size_t)c->n_slots, no = (size_t)sh.n_obs_max;
     const size_t nper = ccdk_period_in_lds() ? 1 : ns * no;  // global period scratch only when not in LDS
     if ((rc = c->s_date.ensure(nper)) || (rc = c->s_row.ensure(nper * 8)) ||
         (rc = c->s_f64.ensure(ns * 8 * no)) || (rc = c->s_bk.ensure(ns * no)))
         return rc;
     if (c->pool_cap < c->total_pix * 8) c->pool_cap = c->total_pix * 8;
     if ((rc = c->pool.ensure(c->pool_cap)) || (rc = c->pool_seq.ensure(c->pool_cap))) return rc;
-    if (dates) HIPCHK(hipMemcpyAsync(c->dates.p, dates, sizeof(int64_t) * nc * no, hipMemcpyHostToDevice, c->stream));
+    // chip tables (pageable sources: the copies are staged before the calls return)
+    HIPCHK(hipMemcpyAsync(c->chip_nobs.p, sh.nobs.data(), sizeof(int32_t) * nc, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->chip_obs_off.p, sh.obs_off.data(), sizeof(int64_t) * (nc + 1), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->chip_pix_off.p, sh.pix_off.data(), sizeof(int64_t) * (nc + 1), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->chip_data_off.p, sh.data_off.data(), sizeof(int64_t) * (nc + 1), hipMemcpyHostToDevice, c->stream));
+    if (dates) HIPCHK(hipMemcpyAsync(c->dates.p, dates, sizeof(int64_t) * tobs, hipMemcpyHostToDevice, c->stream));
     c->in_dates = c->dates.p;
     c->in_spectra = c->spectra.p;
     c->in_qa = c->qa.p;
     return 0;
 }
 
-int ccdgpu_stage(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_chips, int32_t n_pix, int32_t n_obs,
-                 const int64_t *dates, const int16_t *spectra, const uint16_t *qa) {
+static void uniform(int32_t n_chips, int32_t n_pix, int32_t n_obs, std::vector<int32_t> &np, std::vector<int32_t> &no) {
+    np.assign(n_chips > 0 ? n_chips : 0, n_pix);
+    no.assign(n_chips > 0 ? n_chips : 0, n_obs);
+}
+
+int ccdgpu_stage_chips(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_chips, const int32_t *n_pix,
+                       const int32_t *n_obs, const int64_t *dates, const int16_t *spectra, const uint16_t *qa) {
     if (!dates || !spectra || !qa) return fail(CCDGPU_EINVAL, "NULL input buffer");
-    int rc = stage_alloc(c, params, n_chips, n_pix, n_obs, dates);
+    Shape sh;
+    int rc = make_shape(n_chips, n_pix, n_obs, sh);
     if (rc) return rc;
-    const size_t nc = (size_t)n_chips, np = (size_t)n_pix, no = (size_t)n_obs;
-    HIPCHK(hipMemcpyAsync(c->spectra.p, spectra, sizeof(int16_t) * nc * 7 * np * no, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->qa.p, qa, sizeof(uint16_t) * nc * np * no, hipMemcpyHostToDevice, c->stream));
+    if ((rc = stage_alloc(c, params, sh, dates))) return rc;
+    const size_t tdata = (size_t)sh.total_data();
+    HIPCHK(hipMemcpyAsync(c->spectra.p, spectra, sizeof(int16_t) * 7 * tdata, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->qa.p, qa, sizeof(uint16_t) * tdata, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->staged = true;
     c->ran = false;
     return 0;
+}
+
+int ccdgpu_stage(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_chips, int32_t n_pix, int32_t n_obs,
+                 const int64_t *dates, const int16_t *spectra, const uint16_t *qa) {
+    std::vector<int32_t> np, no;
+    uniform(n_chips, n_pix, n_obs, np, no);
+    return ccdgpu_stage_chips(c, params, n_chips, np.data(), no.data(), dates, spectra, qa);
 }
 
 int ccdgpu_stage_chipmunk(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_chips, int32_t n_pix, int32_t n_obs,
@@ -381,16 +434,32 @@ int ccdgpu_stage_chipmunk(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_
                           double *unpack_seconds) {
     if (!dates || !text || !text_offsets || text_bytes < 0) return fail(CCDGPU_EINVAL, "NULL or empty chipmunk text");
     if (n_pix <= 0 || n_pix > (1 << 24)) return fail(CCDGPU_EINVAL, "n_pix out of range");
-    // every present payload must lie inside the text (encoded length incl. '=' padding)
+    if (n_chips <= 0 || n_obs <= 0) return fail(CCDGPU_EINVAL, "n_chips and n_obs must be > 0");
+    // Every present payload is exactly the encoded length of n_pix 16-bit values ('=' padded):
+    // it must lie inside the text and must not run into the next payload (a truncated payload
+    // would otherwise decode its successor's characters as its own tail).
     const int64_t enc = 4 * (((int64_t)2 * n_pix + 2) / 3);
     const int64_t n_off = (int64_t)n_chips * n_obs * 8;
+    std::vector<std::pair<int64_t, int64_t>> present;
+    present.reserve((size_t)n_off);
     for (int64_t i = 0; i < n_off; ++i) {
         const int64_t o = text_offsets[i];
-        if (o >= 0 && o + enc > text_bytes)
+        if (o < 0) continue;
+        if (o + enc > text_bytes)
             return fail(CCDGPU_EINVAL, "chipmunk payload " + std::to_string(i) + " runs past the end of the text");
+        present.emplace_back(o, i);
     }
-    int rc = stage_alloc(c, params, n_chips, n_pix, n_obs, dates);
+    std::sort(present.begin(), present.end());
+    for (size_t k = 0; k + 1 < present.size(); ++k)
+        if (present[k + 1].first - present[k].first < enc)
+            return fail(CCDGPU_EINVAL, "chipmunk payload " + std::to_string(present[k].second) + " is shorter than " +
+                                           std::to_string(enc) + " bytes (" + std::to_string(n_pix) + " values)");
+    std::vector<int32_t> np, no;
+    uniform(n_chips, n_pix, n_obs, np, no);
+    Shape sh;
+    int rc = make_shape(n_chips, np.data(), no.data(), sh);
     if (rc) return rc;
+    if ((rc = stage_alloc(c, params, sh, dates))) return rc;
     if ((rc = c->b64.ensure((size_t)text_bytes + 1)) || (rc = c->b64_off.ensure((size_t)n_off))) return rc;
     HIPCHK(hipMemcpyAsync(c->b64.p, text, (size_t)text_bytes, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->b64_off.p, text_offsets, sizeof(int64_t) * (size_t)n_off, hipMemcpyHostToDevice, c->stream));
@@ -427,39 +496,43 @@ int ccdgpu_host_free(void *ptr) {
     return 0;
 }
 
-int ccdgpu_stage_slot(ccdgpu_ctx *c, int32_t slot, const ccdgpu_params *params, int32_t n_chips, int32_t n_pix,
-                      int32_t n_obs, const int64_t *dates, const int16_t *spectra, const uint16_t *qa) {
+int ccdgpu_stage_slot_chips(ccdgpu_ctx *c, int32_t slot, const ccdgpu_params *params, int32_t n_chips,
+                            const int32_t *n_pix, const int32_t *n_obs, const int64_t *dates, const int16_t *spectra,
+                            const uint16_t *qa) {
     if (!c) return fail(CCDGPU_EINVAL, "NULL ctx");
     if (slot < 0 || slot > 1) return fail(CCDGPU_EINVAL, "slot must be 0 or 1");
     if (!dates || !spectra || !qa) return fail(CCDGPU_EINVAL, "NULL input buffer");
-    if (n_chips <= 0) return fail(CCDGPU_EINVAL, "n_chips must be > 0");
-    int rc = check_params(params, n_pix, n_obs);
-    if (rc) return rc;
+    Shape sh;
+    int rc = make_shape(n_chips, n_pix, n_obs, sh);
+    if (rc || (rc = check_params(params))) return rc;
     HIPCHK(hipSetDevice(c->device));
-    const size_t nc = (size_t)n_chips, np = (size_t)n_pix, no = (size_t)n_obs;
-    if ((rc = c->slot_dates[slot].ensure(nc * no)) || (rc = c->slot_spectra[slot].ensure(nc * 7 * np * no)) ||
-        (rc = c->slot_qa[slot].ensure(nc * np * no)))
+    const size_t tobs = (size_t)sh.total_obs(), tdata = (size_t)sh.total_data();
+    if ((rc = c->slot_dates[slot].ensure(tobs)) || (rc = c->slot_spectra[slot].ensure(7 * tdata)) ||
+        (rc = c->slot_qa[slot].ensure(tdata)))
         return rc;
     // the slot's previous batch was detected by a ccdgpu_run_slot that has returned, so the
     // uploads may overwrite it; they run on the copy stream, concurrent with any detection
-    HIPCHK(hipMemcpyAsync(c->slot_dates[slot].p, dates, sizeof(int64_t) * nc * no, hipMemcpyHostToDevice, c->copy_stream));
-    HIPCHK(hipMemcpyAsync(c->slot_spectra[slot].p, spectra, sizeof(int16_t) * nc * 7 * np * no, hipMemcpyHostToDevice, c->copy_stream));
-    HIPCHK(hipMemcpyAsync(c->slot_qa[slot].p, qa, sizeof(uint16_t) * nc * np * no, hipMemcpyHostToDevice, c->copy_stream));
+    HIPCHK(hipMemcpyAsync(c->slot_dates[slot].p, dates, sizeof(int64_t) * tobs, hipMemcpyHostToDevice, c->copy_stream));
+    HIPCHK(hipMemcpyAsync(c->slot_spectra[slot].p, spectra, sizeof(int16_t) * 7 * tdata, hipMemcpyHostToDevice, c->copy_stream));
+    HIPCHK(hipMemcpyAsync(c->slot_qa[slot].p, qa, sizeof(uint16_t) * tdata, hipMemcpyHostToDevice, c->copy_stream));
     HIPCHK(hipEventRecord(c->uploaded[slot], c->copy_stream));
-    c->slot_shape[slot][0] = n_chips;
-    c->slot_shape[slot][1] = n_pix;
-    c->slot_shape[slot][2] = n_obs;
+    c->slot_shape[slot] = sh;
+    c->slot_params[slot] = *params;  // each slot keeps its own parameters
     c->slot_ready[slot] = true;
-    c->params = *params;
     return 0;
+}
+
+int ccdgpu_stage_slot(ccdgpu_ctx *c, int32_t slot, const ccdgpu_params *params, int32_t n_chips, int32_t n_pix,
+                      int32_t n_obs, const int64_t *dates, const int16_t *spectra, const uint16_t *qa) {
+    std::vector<int32_t> np, no;
+    uniform(n_chips, n_pix, n_obs, np, no);
+    return ccdgpu_stage_slot_chips(c, slot, params, n_chips, np.data(), no.data(), dates, spectra, qa);
 }
 
 int ccdgpu_run_slot(ccdgpu_ctx *c, int32_t slot, double *kernel_seconds) {
     if (!c) return fail(CCDGPU_EINVAL, "NULL ctx");
     if (slot < 0 || slot > 1 || !c->slot_ready[slot]) return fail(CCDGPU_EINVAL, "slot has no staged batch");
-    const ccdgpu_params params = c->params;
-    const int32_t *sh = c->slot_shape[slot];
-    int rc = stage_alloc(c, &params, sh[0], sh[1], sh[2], nullptr, false);
+    int rc = stage_alloc(c, &c->slot_params[slot], c->slot_shape[slot], nullptr, false);
     if (rc) return rc;
     HIPCHK(hipStreamWaitEvent(c->stream, c->uploaded[slot], 0));
     c->in_dates = c->slot_dates[slot].p;
@@ -474,10 +547,10 @@ int ccdgpu_run_slot(ccdgpu_ctx *c, int32_t slot, double *kernel_seconds) {
 int ccdgpu_staged_inputs(ccdgpu_ctx *c, int16_t *spectra, uint16_t *qa) {
     if (!c || !c->staged) return fail(CCDGPU_EINVAL, "nothing staged");
     HIPCHK(hipSetDevice(c->device));
-    const size_t nc = (size_t)c->n_chips, np = (size_t)c->n_pix, no = (size_t)c->n_obs;
+    const size_t tdata = (size_t)c->shape.total_data();
     if (spectra)
-        HIPCHK(hipMemcpyAsync(spectra, c->in_spectra, sizeof(int16_t) * nc * 7 * np * no, hipMemcpyDeviceToHost, c->stream));
-    if (qa) HIPCHK(hipMemcpyAsync(qa, c->in_qa, sizeof(uint16_t) * nc * np * no, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(spectra, c->in_spectra, sizeof(int16_t) * 7 * tdata, hipMemcpyDeviceToHost, c->stream));
+    if (qa) HIPCHK(hipMemcpyAsync(qa, c->in_qa, sizeof(uint16_t) * tdata, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
 }
@@ -486,15 +559,21 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
     if (!c || !c->staged) return fail(CCDGPU_EINVAL, "nothing staged");
     HIPCHK(hipSetDevice(c->device));
     const ccdgpu_params &p = c->params;
+    const Shape &sh = c->shape;
+    const int nc = sh.n_chips();
     CcdDetectArgs a;
     std::memset(&a, 0, sizeof(a));
     a.p = p;
-    a.n_chips = c->n_chips;
-    a.n_pix = c->n_pix;
-    a.n_obs = c->n_obs;
+    a.n_chips = nc;
+    a.n_obs_max = sh.n_obs_max;
     a.mask_words = c->mask_words;
     a.n_slots = c->n_slots;
+    a.poison = c->poison;
     a.total_pix = c->total_pix;
+    a.chip_nobs = c->chip_nobs.p;
+    a.chip_obs_off = c->chip_obs_off.p;
+    a.chip_pix_off = c->chip_pix_off.p;
+    a.chip_data_off = c->chip_data_off.p;
     a.spectra = c->in_spectra;
     a.qa = c->in_qa;
     a.order = c->order.p;
@@ -518,15 +597,16 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         a.pool = c->pool.p;
         a.pool_seq = c->pool_seq.p;
         a.pool_cap = c->pool_cap;
-        unsigned long long init[8] = {0ull, 0ull, ~0ull, 0ull, 0ull, ~0ull, 0ull, 0ull};
+        unsigned long long init[8] = {0ull, 0ull, ~0ull, 0ull, 0ull, ~0ull, 0ull, ~0ull};
         HIPCHK(hipMemcpyAsync(c->counters.p, init, sizeof(init), hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipMemsetAsync(c->stats.p, 0, sizeof(unsigned long long) * CCD_NSTATS, c->stream));
         if (ccdk_set_args(&a, c->arg_slot, c->stream)) return fail(CCDGPU_EHIP, "copying kernel arguments to constant memory failed");
         HIPCHK(hipEventRecord(c->ev[0], c->stream));
-        if (ccdk_prep(c->in_dates, c->n_chips, c->n_obs, p.avg_days_yr, c->order.p, c->sdates.p, c->basis.p, c->stream))
+        if (ccdk_prep(c->in_dates, nc, c->chip_nobs.p, c->chip_obs_off.p, p.avg_days_yr, c->order.p, c->sdates.p, c->basis.p,
+                      c->stream))
             return fail(CCDGPU_EHIP, std::string("prep launch: ") + hipGetErrorString(hipGetLastError()));
         HIPCHK(hipEventRecord(c->ev[1], c->stream));
-        if (ccdk_detect(c->n_slots, c->variant, c->n_obs, c->arg_slot, c->stream))
+        if (ccdk_detect(c->n_slots, c->variant, sh.n_obs_max, c->arg_slot, c->stream))
             return fail(CCDGPU_EHIP, std::string("detect launch: ") + hipGetErrorString(hipGetLastError()));
         HIPCHK(hipEventRecord(c->ev[2], c->stream));
         unsigned long long h[8];
@@ -558,7 +638,7 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         HIPCHK(hipMemcpyAsync(c->h_offsets.data(), c->offsets.p, sizeof(int64_t) * c->total_pix, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         c->h_offsets[c->total_pix] = c->n_pool;
-        if (ccdk_scatter(c->pool.p, c->pool_seq.p, c->n_pool, c->offsets.p, c->n_pix, c->csr.p, c->stream))
+        if (ccdk_scatter(c->pool.p, c->pool_seq.p, c->n_pool, c->offsets.p, c->chip_pix_off.p, nc, c->csr.p, c->stream))
             return fail(CCDGPU_EHIP, "scatter launch failed");
         HIPCHK(hipEventRecord(c->ev[3], c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
@@ -570,11 +650,15 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         c->last.lasso_fits = (int64_t)st[0];
         c->last.cd_sweeps = (int64_t)st[1];
         c->last.flops = (int64_t)st[2];
-        const int64_t in_bytes = c->total_pix * (int64_t)c->n_obs * 16 + (int64_t)c->n_chips * c->n_obs * 8;
+        const int64_t in_bytes = sh.total_data() * 16 + sh.total_obs() * 8;
         const int64_t out_bytes = c->n_pool * (int64_t)sizeof(ccdgpu_segment) + c->total_pix * ((int64_t)c->mask_words * 4 + 4 + 24 + 4);
         c->last.bytes = in_bytes + out_bytes;
         if (kernel_seconds) *kernel_seconds = (ms_prep + ms_det) * 1e-3;
         c->ran = true;
+        if (h[7] != ~0ull)
+            return fail(CCDGPU_EOVERFLOW, "adaptive peek of pixel " + std::to_string(h[7]) + " exceeds " +
+                                              std::to_string(CCDGPU_MAX_PEEK) + " observations (PEEK_SIZE " +
+                                              std::to_string(p.peek_size) + ")");
         if (h[2] != ~0ull) {
             g_err = "unsupported bit-packed QA value (pixel " + std::to_string(h[2]) + ")";
             return CCDGPU_EQA;
@@ -599,10 +683,10 @@ int ccdgpu_last_stats(ccdgpu_ctx *c, ccdgpu_stats *s) {
 static int fetch_chip(ccdgpu_ctx *c, int32_t chip, ccdgpu_result *out) {
     std::memset(out, 0, sizeof(*out));
     if (!c->ran) return fail(CCDGPU_EINVAL, "no completed run to fetch");
-    if (chip < 0 || chip >= c->n_chips) return fail(CCDGPU_EINVAL, "chip index out of range");
+    if (chip < 0 || chip >= c->shape.n_chips()) return fail(CCDGPU_EINVAL, "chip index out of range");
     HIPCHK(hipSetDevice(c->device));
-    const int np = c->n_pix, no = c->n_obs;
-    const int64_t p0 = (int64_t)chip * np;
+    const int np = c->shape.npix[chip], no = c->shape.nobs[chip];
+    const int64_t p0 = c->shape.pix_off[chip], o0 = c->shape.obs_off[chip];
     const int64_t s0 = c->h_offsets[p0], s1 = c->h_offsets[p0 + np];
     out->n_pix = np;
     out->n_obs = no;
@@ -627,8 +711,8 @@ static int fetch_chip(ccdgpu_ctx *c, int32_t chip, ccdgpu_result *out) {
     HIPCHK(hipMemcpyAsync(out->mask_bits, c->mask.p + (size_t)p0 * c->mask_words, sizeof(uint32_t) * (size_t)np * c->mask_words, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(out->procedure, c->procedure.p + p0, sizeof(int32_t) * np, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(out->probs, c->probs.p + 3 * p0, sizeof(double) * 3 * np, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(out->sorted_dates, c->sdates.p + (size_t)chip * no, sizeof(int64_t) * no, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(out->sort_index, c->order.p + (size_t)chip * no, sizeof(int32_t) * no, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(out->sorted_dates, c->sdates.p + o0, sizeof(int64_t) * no, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(out->sort_index, c->order.p + o0, sizeof(int32_t) * no, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     for (int i = 0; i < np; ++i)
         if (out->procedure[i] < 0) {
@@ -638,46 +722,71 @@ static int fetch_chip(ccdgpu_ctx *c, int32_t chip, ccdgpu_result *out) {
     return 0;
 }
 
-int ccdgpu_fetch_rows(ccdgpu_ctx *c, int32_t chip, int32_t cx, int32_t cy, int32_t width, ccdgpu_rows *out) {
-    if (!c || !out) return fail(CCDGPU_EINVAL, "NULL argument");
+// Rows of chips [c0, c1) of the last run, packed on the device and copied back in one piece:
+// row offsets over the chips' pixels, rows pixel-major, masks one byte per date (chip c's block at
+// data_off[c] - data_off[c0], [n_pix_c][n_obs_c]).
+static int fetch_rows_range(ccdgpu_ctx *c, int32_t c0, int32_t c1, const int32_t *cx, const int32_t *cy, int32_t width,
+                            ccdgpu_rows *out) {
     std::memset(out, 0, sizeof(*out));
     if (!c->ran) return fail(CCDGPU_EINVAL, "no completed run to fetch");
-    if (chip < 0 || chip >= c->n_chips) return fail(CCDGPU_EINVAL, "chip index out of range");
     if (width <= 0) return fail(CCDGPU_EINVAL, "width must be > 0");
     HIPCHK(hipSetDevice(c->device));
-    const int np = c->n_pix, no = c->n_obs;
-    const int64_t p0 = (int64_t)chip * np;
+    const Shape &sh = c->shape;
+    const int64_t p0 = sh.pix_off[c0], np = sh.pix_off[c1] - p0;
+    const int64_t d0 = sh.data_off[c0], nd = sh.data_off[c1] - d0;
     const int64_t s0 = c->h_offsets[p0];
     // rows per pixel = max(1, segments): host prefix over the segment offsets already here
-    std::vector<int64_t> soff(np + 1), roff(np + 1);
+    std::vector<int64_t> soff((size_t)np + 1), roff((size_t)np + 1);
     roff[0] = 0;
-    for (int i = 0; i <= np; ++i) soff[i] = c->h_offsets[p0 + i] - s0;
-    for (int i = 0; i < np; ++i) roff[i + 1] = roff[i] + std::max<int64_t>(1, soff[i + 1] - soff[i]);
+    for (int64_t i = 0; i <= np; ++i) soff[i] = c->h_offsets[p0 + i] - s0;
+    for (int64_t i = 0; i < np; ++i) roff[i + 1] = roff[i] + std::max<int64_t>(1, soff[i + 1] - soff[i]);
     const int64_t n_rows = roff[np];
     int rc;
     if ((rc = c->rows.ensure((size_t)n_rows)) || (rc = c->row_off.ensure(np + 1)) || (rc = c->seg_off1.ensure(np + 1)) ||
-        (rc = c->mask8.ensure((size_t)np * no)))
+        (rc = c->mask8.ensure((size_t)nd)))
         return rc;
     HIPCHK(hipMemcpyAsync(c->seg_off1.p, soff.data(), sizeof(int64_t) * (np + 1), hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->row_off.p, roff.data(), sizeof(int64_t) * (np + 1), hipMemcpyHostToDevice, c->stream));
-    if (ccdk_pack_rows(c->csr.p + s0, c->seg_off1.p, c->row_off.p, c->mask.p + (size_t)p0 * c->mask_words, c->mask_words,
-                       np, no, cx, cy, width, c->rows.p, c->mask8.p, c->stream))
-        return fail(CCDGPU_EHIP, "row packing launch failed");
-    out->n_pix = np;
-    out->n_obs = no;
+    for (int32_t ch = c0; ch < c1; ++ch) {
+        const int64_t q = sh.pix_off[ch] - p0;
+        if (ccdk_pack_rows(c->csr.p + s0, c->seg_off1.p + q, c->row_off.p + q, c->mask.p + (size_t)sh.pix_off[ch] * c->mask_words,
+                           c->mask_words, sh.npix[ch], sh.nobs[ch], cx[ch - c0], cy[ch - c0], width, c->rows.p,
+                           c->mask8.p + (sh.data_off[ch] - d0), c->stream))
+            return fail(CCDGPU_EHIP, "row packing launch failed");
+    }
+    out->n_pix = (int32_t)np;
+    out->n_obs = c1 - c0 == 1 ? sh.nobs[c0] : 0;
     out->n_rows = n_rows;
     out->row_offsets = (int64_t *)std::malloc(sizeof(int64_t) * (np + 1));
-    out->rows = (ccdgpu_row *)std::malloc(sizeof(ccdgpu_row) * (size_t)n_rows);
-    out->mask = (int8_t *)std::malloc((size_t)np * no);
+    out->rows = (ccdgpu_row *)std::malloc(sizeof(ccdgpu_row) * (size_t)(n_rows > 0 ? n_rows : 1));
+    out->mask = (int8_t *)std::malloc((size_t)(nd > 0 ? nd : 1));
     if (!out->row_offsets || !out->rows || !out->mask) {
         ccdgpu_rows_free(out);
         return fail(CCDGPU_ENOMEM, "host allocation failed");
     }
     std::memcpy(out->row_offsets, roff.data(), sizeof(int64_t) * (np + 1));
     HIPCHK(hipMemcpyAsync(out->rows, c->rows.p, sizeof(ccdgpu_row) * (size_t)n_rows, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(out->mask, c->mask8.p, (size_t)np * no, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(out->mask, c->mask8.p, (size_t)nd, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
+}
+
+int ccdgpu_fetch_rows(ccdgpu_ctx *c, int32_t chip, int32_t cx, int32_t cy, int32_t width, ccdgpu_rows *out) {
+    if (!c || !out) return fail(CCDGPU_EINVAL, "NULL argument");
+    if (chip < 0 || chip >= c->shape.n_chips()) {
+        std::memset(out, 0, sizeof(*out));
+        return fail(CCDGPU_EINVAL, "chip index out of range");
+    }
+    return fetch_rows_range(c, chip, chip + 1, &cx, &cy, width, out);
+}
+
+int ccdgpu_fetch_batch_rows(ccdgpu_ctx *c, const int32_t *cx, const int32_t *cy, int32_t width, ccdgpu_rows *out) {
+    if (!c || !out || !cx || !cy) return fail(CCDGPU_EINVAL, "NULL argument");
+    if (c->shape.n_chips() <= 0) {
+        std::memset(out, 0, sizeof(*out));
+        return fail(CCDGPU_EINVAL, "no completed run to fetch");
+    }
+    return fetch_rows_range(c, 0, c->shape.n_chips(), cx, cy, width, out);
 }
 
 void ccdgpu_rows_free(ccdgpu_rows *r) {

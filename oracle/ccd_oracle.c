@@ -50,6 +50,7 @@ typedef struct {
     int *idx;            /* compacted indices (period) */
     int m;
     int peek;
+    int overflow; /* adaptive peek exceeded CCDGPU_MAX_PEEK */
     double chg_thr;
     double vario[NB];
     /* scratch */
@@ -603,6 +604,9 @@ static void standard_procedure(pix_t *P) {
         free(d);
         double adj = rint((double)p->peek_size * 16.0 / delta);
         if (adj > p->peek_size) {
+            /* as the kernel (include/ccdgpu.h CCDGPU_MAX_PEEK): a peek past 96 is reported
+               (CCDGPU_EOVERFLOW), the pixel finishes with the largest supported peek */
+            if (adj > CCDGPU_MAX_PEEK) P->overflow = 1;
             P->peek = adj > CCDGPU_MAX_PEEK ? CCDGPU_MAX_PEEK : (int)adj;
             double pt = 1.0 - pow(1.0 - p->change_probability, (double)p->peek_size / P->peek);
             P->chg_thr = chi2_5_ppf(pt);
@@ -739,6 +743,7 @@ static int detect_pixel(const ccdgpu_params *p, int n, const int64_t *t, const d
         free(P.X); free(P.Xc); free(P.yc); free(P.y); free(P.R); free(P.resid_store);
     }
 done:
+    if (!rc && P.overflow) rc = CCDGPU_EOVERFLOW;
     *segs = P.segs;
     *nseg = P.nseg;
     *fits += P.fits;
@@ -774,7 +779,8 @@ void ccdoracle_params_default(ccdgpu_params *p) {
 
 double ccdoracle_chi2_5_ppf(double p) { return chi2_5_ppf(p); }
 
-/* Same layout contract as ccdgpu_detect_batch (include/ccdgpu.h). Returns 0 or CCDGPU_EQA. */
+/* Same layout contract as ccdgpu_detect_batch (include/ccdgpu.h). Returns 0, CCDGPU_EOVERFLOW (a
+   pixel's adaptive peek exceeds CCDGPU_MAX_PEEK) or CCDGPU_EQA. */
 int ccdoracle_detect_batch(const ccdgpu_params *p, int32_t n_pix, int32_t n_obs, const int64_t *dates,
                            const int16_t *spectra, const uint16_t *qa, ccdgpu_result *out, int32_t n_threads) {
     memset(out, 0, sizeof(*out));
@@ -804,7 +810,7 @@ int ccdoracle_detect_batch(const ccdgpu_params *p, int32_t n_pix, int32_t n_obs,
     out->seg_offsets = (int64_t *)calloc((size_t)n_pix + 1, sizeof(int64_t));
     ccdgpu_segment **psegs = (ccdgpu_segment **)calloc((size_t)n_pix + 1, sizeof(void *));
     int *pn = (int *)calloc((size_t)n_pix + 1, sizeof(int));
-    int err_pix = -1;
+    int err_pix = -1, ovf_pix = -1;
     int64_t fits = 0, sweeps = 0;
     (void)n_threads;
 #pragma omp parallel for schedule(dynamic, 1) num_threads(n_threads > 0 ? n_threads : 1) reduction(+ : fits, sweeps)
@@ -814,9 +820,12 @@ int ccdoracle_detect_batch(const ccdgpu_params *p, int32_t n_pix, int32_t n_obs,
                               (size_t)n_pix * n_obs, &psegs[px], &pn[px],
                               out->mask_bits + (size_t)px * out->mask_words, &out->procedure[px],
                               out->probs + 3 * (size_t)px, &fits, &sweeps);
-        if (rc) {
+        if (rc == CCDGPU_EQA) {
 #pragma omp critical
             if (err_pix < 0 || px < err_pix) err_pix = px;
+        } else if (rc == CCDGPU_EOVERFLOW) {
+#pragma omp critical
+            if (ovf_pix < 0 || px < ovf_pix) ovf_pix = px;
         }
     }
     int64_t tot = 0;
@@ -835,6 +844,7 @@ int ccdoracle_detect_batch(const ccdgpu_params *p, int32_t n_pix, int32_t n_obs,
     out->error_pixel = err_pix;
     out->seconds_kernel = (double)fits;   /* oracle: reports fit/sweep counters here */
     out->seconds_total = (double)sweeps;
+    if (ovf_pix >= 0) return CCDGPU_EOVERFLOW;
     return err_pix >= 0 ? CCDGPU_EQA : 0;
 }
 

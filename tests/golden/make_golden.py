@@ -3,6 +3,7 @@ of lcmap-pyccd ccd.detect).  Inputs come from the synthetic ARD generator (libcc
 hand-built edge cases; expected outputs are the restatement's change models and masks.
 
     python tests/golden/make_golden.py            # ~1 min on 8 cores
+    python tests/golden/make_golden.py dense_daily # one case
 
 The reference itself (lcmap-pyccd) is not importable in this container, so these
 vectors pin the GPU path and the C oracle to the restatement; the restatement is pinned by the
@@ -105,7 +106,21 @@ def edge_cases():
     return cases
 
 
+def dense_case():
+    """Daily acquisitions for five years with few clouds: the filtered dates' median gap is 1
+    day, so the ncompare peek is round(6 * 16 / 1) = 96 (CCDGPU_MAX_PEEK; larger than the 64-row
+    lookforward batch) and the change threshold chi2.ppf(1 - 0.01^(6/96), 5); breaks every 3
+    years.  Pixel 3 thins its clear days to every other one (peek 48)."""
+    d = np.arange(730120, 730120 + 1826, dtype=np.int64)[::-1].copy()
+    cfg = synth.config(5, p_clear=0.93, p_cloud=0.02, p_shadow=0.01, p_snow=0.01, p_water=0.01, p_fill=0.02)
+    _, s, q = synth.chip(cfg, 7, 0, 6, chip_dates=d)
+    q = q.copy()
+    q[3, 1::2] = 224  # every other day cloudy
+    return d, s, q
+
+
 def main():
+    only = set(sys.argv[1:])
     cases = {
         'c2_chip11': (synth_case(2, 11, 16), None),
         'c4_chip11': (synth_case(4, 11, 16), None),
@@ -116,8 +131,11 @@ def main():
     }
     for name, inp in edge_cases().items():
         cases[name] = (inp, None)
+    cases['dense_daily'] = (dense_case(), None)
     with multiprocessing.Pool(min(8, os.cpu_count() or 1)) as pool:
         for name, ((d, s, q), params) in cases.items():
+            if only and name not in only:
+                continue
             jobs = [(d, s[:, p], q[p], params) for p in range(q.shape[0])]
             results = pool.map(run_pixel, jobs)
             out = to_arrays(results, d.shape[0])

@@ -80,3 +80,13 @@ def test_oracle_unsupported_qa_is_an_error():
     q[1, 17] = 64  # only bit 6 set: pyccd qa.qabitval raises ValueError
     rc, u = oracle_ctypes.detect_batch(d, s, q, threads=2)
     assert rc == abi.E_QA and u.error_pixel == 1
+
+
+def test_oracle_peek_overflow_is_an_error():
+    """An adaptive peek past CCDGPU_MAX_PEEK (96; only reachable with PEEK_SIZE > 6 on dense
+    dates) is CCDGPU_EOVERFLOW, as on the GPU; the default PEEK_SIZE on daily dates (peek 96)
+    is supported and matches the golden (test_c_oracle_matches_golden[dense_daily])."""
+    (d, s, q), _, _ = golden_util.load('dense_daily')
+    rc, _ = oracle_ctypes.detect_batch(d, s[:, :2], q[:2], params={'PEEK_SIZE': 8}, threads=2)
+    assert rc == abi.E_OVERFLOW
+    assert abi.MAX_PEEK == 96

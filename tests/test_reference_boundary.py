@@ -151,14 +151,16 @@ def test_detect_partition_batches_and_matches_per_pixel(monkeypatch):
     import ccd
     from ccdgpu import synth
 
-    def fake_batch(dates, spectra, qas, params=None):
-        return [ccd_ref.detect(dates, *[spectra[b, i] for b in range(7)], qas[i], params=params)
-                for i in range(qas.shape[0])]
+    def fake_groups(groups, params=None):
+        return [[ccd_ref.detect(dates, *[spectra[b, i] for b in range(7)], qas[i], params=params)
+                 for i in range(qas.shape[0])] for dates, spectra, qas in groups]
 
-    monkeypatch.setattr(ccd, 'detect_batch', fake_batch)
+    monkeypatch.setattr(ccd, 'detect_groups', fake_groups)
     monkeypatch.setattr(ccd, 'detect', ccd_ref.detect)
     d, s, q = synth.chip(synth.config(2), 9, 0, 3)
-    recs = timeseries.unpack(timeseries.chip_keys(0, 0, 3), d, s, q) + [TIMESERIES_ELEMENT]
+    d3, s3, q3 = synth.chip(synth.config(3), 1, 0, 2)  # a sidelap chip: another date vector
+    recs = (timeseries.unpack(timeseries.chip_keys(0, 0, 3), d, s, q) + [TIMESERIES_ELEMENT] +
+            timeseries.unpack(timeseries.chip_keys(3000, 0, 2), d3, s3, q3))
     rows = pyccd.detect_partition(recs)
     expected = [row for rec in recs for row in pyccd.detect(rec)]
     assert len(rows) == len(expected)
