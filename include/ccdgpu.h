@@ -122,7 +122,10 @@ typedef struct ccdgpu_rows {
     int64_t *row_offsets;       /* [n_pix + 1]                                             */
     ccdgpu_row *rows;           /* [n_rows], pixel-major                                   */
     int8_t *mask;               /* [n_pix][n_obs] processing mask 0/1, sorted date order   */
-                                /* (pixel table, resources/schema.cql pixel.mask)          */
+                                /* (pixel table, resources/schema.cql pixel.mask); NULL    */
+                                /* for a batch fetch, which returns mask_bits instead      */
+    uint32_t *mask_bits;        /* batch fetch: [n_pix][mask_words] the same mask as bits  */
+    int32_t mask_words;         /* (bit i of word i/32 = sorted observation i), 8x smaller */
 } ccdgpu_rows;
 
 typedef struct ccdgpu_ctx ccdgpu_ctx;
@@ -209,8 +212,9 @@ int ccdgpu_fetch_staged(ccdgpu_ctx *ctx, int32_t chip, ccdgpu_result *out);
  * Replaces the per-segment Python formatting of ccdc/pyccd.py:106-148 + Spark's float cast. */
 int ccdgpu_fetch_rows(ccdgpu_ctx *ctx, int32_t chip, int32_t cx, int32_t cy, int32_t width, ccdgpu_rows *out);
 /* The same for every chip of the batch in one device pass and one copy (the tile runner's
- * gather): chip c at (cx[c], cy[c]); row_offsets over all pixels of the batch; mask of chip c
- * at byte D_c (ccdgpu_stage_chips), [n_pix[c]][n_obs[c]]; out->n_obs is 0 for a multi-chip batch. */
+ * gather): chip c at (cx[c], cy[c]); row_offsets over all pixels of the batch; the masks come
+ * back bit-packed (out->mask_bits [n_pix of the batch][out->mask_words], out->mask NULL);
+ * out->n_obs is 0 for a multi-chip batch. */
 int ccdgpu_fetch_batch_rows(ccdgpu_ctx *ctx, const int32_t *cx, const int32_t *cy, int32_t width, ccdgpu_rows *out);
 void ccdgpu_rows_free(ccdgpu_rows *out);
 

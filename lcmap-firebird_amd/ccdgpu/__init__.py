@@ -176,10 +176,15 @@ class ChipBatch(object):
             b.set_chip(i, d, s, q)
         return b
 
-    def mask_of(self, mask, c):
-        """Chip c's [n_pix][n_obs] block of a batch row fetch's flat mask."""
-        npx, n, d = int(self.n_pix[c]), int(self.n_obs[c]), int(self.data_off[c])
-        return mask[d:d + npx * n].reshape(npx, n)
+    def mask_of(self, bits, c):
+        """Chip c's int8 [n_pix][n_obs] processing mask from a batch row fetch's bit words."""
+        p0, p1 = int(self.pix_off[c]), int(self.pix_off[c + 1])
+        return abi.unpack_mask_bits(bits[p0:p1], int(self.n_obs[c]))
+
+    def mask_bits_of(self, bits, c):
+        """Chip c's bit words of a batch row fetch, [n_pix][ceil(n_obs / 32)] (no unpacking;
+        the batch's own word count, set by its largest chip, is trimmed to the chip's)."""
+        return bits[int(self.pix_off[c]):int(self.pix_off[c + 1]), :(int(self.n_obs[c]) + 31) // 32]
 
 
 def _as_inputs(dates, spectra, qa):
@@ -193,6 +198,7 @@ class Context(object):
     """One HIP device + stream (ccdgpu_ctx).  Not shared across threads."""
 
     def __init__(self, device=0):
+        self.qa_error = False
         self._ctx = ctypes.c_void_p()
         _check(lib().ccdgpu_init(int(device), ctypes.byref(self._ctx)))
         self.device = device
@@ -273,8 +279,8 @@ class Context(object):
 
     def fetch_batch_rows(self, cx, cy, width=100):
         """Rows of every chip of the last run in one device pass and one copy: (row_offsets
-        [total_pixels+1], rows abi.ROW_DTYPE, mask int8 flat in the ChipBatch data layout --
-        ChipBatch.mask_of(mask, c) is chip c's [n_pix][n_obs] block)."""
+        [total_pixels+1], rows abi.ROW_DTYPE, mask bit words uint32 [total_pixels][words] --
+        ChipBatch.mask_of(bits, c) is chip c's int8 [n_pix][n_obs] mask)."""
         batch = self._keep
         if not isinstance(batch, ChipBatch):
             raise ValueError('fetch_batch_rows needs a stage_chips / stage_slot_chips batch')
@@ -286,7 +292,7 @@ class Context(object):
         rc = lib().ccdgpu_fetch_batch_rows(self._ctx, cx.ctypes.data, cy.ctypes.data, int(width), ctypes.byref(r))
         try:
             _check(rc)
-            return abi.unpack_rows(r, mask_len=int(batch.data_off[-1]))
+            return abi.unpack_rows(r)
         finally:
             lib().ccdgpu_rows_free(ctypes.byref(r))
 
@@ -310,6 +316,7 @@ class Context(object):
         rc = lib().ccdgpu_run_slot(self._ctx, int(slot), ctypes.byref(secs))
         if rc not in (0, abi.E_QA):
             _check(rc)
+        self.qa_error = rc == abi.E_QA  # results exist; the pixel's procedure is -1 (fetch)
         self._keep = self._slot_keep.get(int(slot))
         self._n_pix = None if isinstance(self._keep, ChipBatch) else self._keep[2].shape[1]
         return secs.value
@@ -359,6 +366,7 @@ class Context(object):
         rc = lib().ccdgpu_run_staged(self._ctx, ctypes.byref(secs))
         if rc not in (0, abi.E_QA):
             _check(rc)
+        self.qa_error = rc == abi.E_QA  # results exist; the pixel's procedure is -1 (fetch)
         return secs.value
 
     def fetch(self, chip):

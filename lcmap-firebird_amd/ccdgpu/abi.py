@@ -81,20 +81,32 @@ class Rows(ctypes.Structure):
         ('row_offsets', ctypes.POINTER(ctypes.c_int64)),
         ('rows', ctypes.POINTER(Row)),
         ('mask', ctypes.POINTER(ctypes.c_int8)),
+        ('mask_bits', ctypes.POINTER(_u32)),
+        ('mask_words', _i32),
     ]
 
 
-def unpack_rows(r, mask_len=None):
-    """ccdgpu_rows -> (row_offsets [n_pix+1], rows ROW_DTYPE [n_rows], mask int8 [n_pix][n_obs]
-    -- or, with mask_len, the flat mask of a batch fetch), copied out of library memory."""
+def unpack_rows(r):
+    """ccdgpu_rows -> (row_offsets [n_pix+1], rows ROW_DTYPE [n_rows], mask), copied out of
+    library memory; mask is int8 [n_pix][n_obs] for a chip fetch, the bit words uint32
+    [n_pix][mask_words] for a batch fetch (ccdgpu_fetch_batch_rows)."""
     n_pix, n_obs, n = r.n_pix, r.n_obs, r.n_rows
     off = np.ctypeslib.as_array(r.row_offsets, shape=(n_pix + 1,)).copy()
     rows = np.frombuffer(ctypes.string_at(ctypes.cast(r.rows, ctypes.c_void_p), n * ROW_DTYPE.itemsize),
                          dtype=ROW_DTYPE).copy() if n else np.zeros(0, ROW_DTYPE)
-    if mask_len is not None:
-        return off, rows, np.ctypeslib.as_array(r.mask, shape=(max(int(mask_len), 1),))[:int(mask_len)].copy()
+    if bool(r.mask_bits):
+        w = r.mask_words
+        bits = np.ctypeslib.as_array(r.mask_bits, shape=(max(n_pix * w, 1),))[:n_pix * w].reshape(n_pix, w).copy()
+        return off, rows, bits
     mask = np.ctypeslib.as_array(r.mask, shape=(n_pix, n_obs)).copy()
     return off, rows, mask
+
+
+def unpack_mask_bits(bits, n_obs):
+    """[n_pix][mask_words] uint32 mask words -> int8 [n_pix][n_obs] (bit i of word i/32)."""
+    b = np.ascontiguousarray(bits, dtype='<u4')
+    u8 = np.unpackbits(b.view(np.uint8).reshape(b.shape[0], -1), axis=1, bitorder='little')
+    return u8[:, :n_obs].astype(np.int8)
 
 
 class Result(ctypes.Structure):

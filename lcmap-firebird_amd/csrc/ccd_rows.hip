@@ -60,7 +60,9 @@ __global__ __launch_bounds__(256) void ccd_pack_rows(const ccdgpu_segment *__res
             }
             rows[r0 + j] = r;
         }
-        // pixel table: processing mask, one byte per date (sorted order)
+        // pixel table: processing mask, one byte per date (sorted order); skipped when the
+        // caller fetches the bit-packed mask instead
+        if (!mask) continue;
         const uint32_t *mb = mask_bits + (int64_t)p * mask_words;
         int8_t *mo = mask + (int64_t)p * n_obs;
         for (int i = l; i < n_obs; i += W) mo[i] = (int8_t)((mb[i >> 5] >> (i & 31)) & 1u);

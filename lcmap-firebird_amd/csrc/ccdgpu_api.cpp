@@ -723,10 +723,11 @@ static int fetch_chip(ccdgpu_ctx *c, int32_t chip, ccdgpu_result *out) {
 }
 
 // Rows of chips [c0, c1) of the last run, packed on the device and copied back in one piece:
-// row offsets over the chips' pixels, rows pixel-major, masks one byte per date (chip c's block at
-// data_off[c] - data_off[c0], [n_pix_c][n_obs_c]).
+// row offsets over the chips' pixels, rows pixel-major, and the masks either one byte per date
+// (packed_mask false: chip c's block at data_off[c] - data_off[c0], [n_pix_c][n_obs_c]) or as the
+// device's bit words ([pixels][mask_words]).
 static int fetch_rows_range(ccdgpu_ctx *c, int32_t c0, int32_t c1, const int32_t *cx, const int32_t *cy, int32_t width,
-                            ccdgpu_rows *out) {
+                            ccdgpu_rows *out, bool packed_mask) {
     std::memset(out, 0, sizeof(*out));
     if (!c->ran) return fail(CCDGPU_EINVAL, "no completed run to fetch");
     if (width <= 0) return fail(CCDGPU_EINVAL, "width must be > 0");
@@ -743,7 +744,7 @@ static int fetch_rows_range(ccdgpu_ctx *c, int32_t c0, int32_t c1, const int32_t
     const int64_t n_rows = roff[np];
     int rc;
     if ((rc = c->rows.ensure((size_t)n_rows)) || (rc = c->row_off.ensure(np + 1)) || (rc = c->seg_off1.ensure(np + 1)) ||
-        (rc = c->mask8.ensure((size_t)nd)))
+        (!packed_mask && (rc = c->mask8.ensure((size_t)nd))))
         return rc;
     HIPCHK(hipMemcpyAsync(c->seg_off1.p, soff.data(), sizeof(int64_t) * (np + 1), hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->row_off.p, roff.data(), sizeof(int64_t) * (np + 1), hipMemcpyHostToDevice, c->stream));
@@ -751,7 +752,7 @@ static int fetch_rows_range(ccdgpu_ctx *c, int32_t c0, int32_t c1, const int32_t
         const int64_t q = sh.pix_off[ch] - p0;
         if (ccdk_pack_rows(c->csr.p + s0, c->seg_off1.p + q, c->row_off.p + q, c->mask.p + (size_t)sh.pix_off[ch] * c->mask_words,
                            c->mask_words, sh.npix[ch], sh.nobs[ch], cx[ch - c0], cy[ch - c0], width, c->rows.p,
-                           c->mask8.p + (sh.data_off[ch] - d0), c->stream))
+                           packed_mask ? nullptr : c->mask8.p + (sh.data_off[ch] - d0), c->stream))
             return fail(CCDGPU_EHIP, "row packing launch failed");
     }
     out->n_pix = (int32_t)np;
@@ -759,14 +760,24 @@ static int fetch_rows_range(ccdgpu_ctx *c, int32_t c0, int32_t c1, const int32_t
     out->n_rows = n_rows;
     out->row_offsets = (int64_t *)std::malloc(sizeof(int64_t) * (np + 1));
     out->rows = (ccdgpu_row *)std::malloc(sizeof(ccdgpu_row) * (size_t)(n_rows > 0 ? n_rows : 1));
-    out->mask = (int8_t *)std::malloc((size_t)(nd > 0 ? nd : 1));
-    if (!out->row_offsets || !out->rows || !out->mask) {
+    const size_t nbits = (size_t)np * c->mask_words;
+    if (packed_mask) {
+        out->mask_words = c->mask_words;
+        out->mask_bits = (uint32_t *)std::malloc(sizeof(uint32_t) * (nbits > 0 ? nbits : 1));
+    } else {
+        out->mask = (int8_t *)std::malloc((size_t)(nd > 0 ? nd : 1));
+    }
+    if (!out->row_offsets || !out->rows || (packed_mask ? !out->mask_bits : !out->mask)) {
         ccdgpu_rows_free(out);
         return fail(CCDGPU_ENOMEM, "host allocation failed");
     }
     std::memcpy(out->row_offsets, roff.data(), sizeof(int64_t) * (np + 1));
     HIPCHK(hipMemcpyAsync(out->rows, c->rows.p, sizeof(ccdgpu_row) * (size_t)n_rows, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(out->mask, c->mask8.p, (size_t)nd, hipMemcpyDeviceToHost, c->stream));
+    if (packed_mask)
+        HIPCHK(hipMemcpyAsync(out->mask_bits, c->mask.p + (size_t)p0 * c->mask_words, sizeof(uint32_t) * nbits,
+                              hipMemcpyDeviceToHost, c->stream));
+    else
+        HIPCHK(hipMemcpyAsync(out->mask, c->mask8.p, (size_t)nd, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
 }
@@ -777,7 +788,7 @@ int ccdgpu_fetch_rows(ccdgpu_ctx *c, int32_t chip, int32_t cx, int32_t cy, int32
         std::memset(out, 0, sizeof(*out));
         return fail(CCDGPU_EINVAL, "chip index out of range");
     }
-    return fetch_rows_range(c, chip, chip + 1, &cx, &cy, width, out);
+    return fetch_rows_range(c, chip, chip + 1, &cx, &cy, width, out, false);
 }
 
 int ccdgpu_fetch_batch_rows(ccdgpu_ctx *c, const int32_t *cx, const int32_t *cy, int32_t width, ccdgpu_rows *out) {
@@ -786,7 +797,7 @@ int ccdgpu_fetch_batch_rows(ccdgpu_ctx *c, const int32_t *cx, const int32_t *cy,
         std::memset(out, 0, sizeof(*out));
         return fail(CCDGPU_EINVAL, "no completed run to fetch");
     }
-    return fetch_rows_range(c, 0, c->shape.n_chips(), cx, cy, width, out);
+    return fetch_rows_range(c, 0, c->shape.n_chips(), cx, cy, width, out, true);
 }
 
 void ccdgpu_rows_free(ccdgpu_rows *r) {
@@ -794,6 +805,7 @@ void ccdgpu_rows_free(ccdgpu_rows *r) {
     std::free(r->row_offsets);
     std::free(r->rows);
     std::free(r->mask);
+    std::free(r->mask_bits);
     std::memset(r, 0, sizeof(*r));
 }
 

@@ -1,0 +1,89 @@
+"""Host restatement of the device row writer (lcmap-firebird_amd/csrc/ccd_rows.hip) over an
+abi.Unpacked result -- test infrastructure for the tile runner's CPU tests (an oracle-backed
+stand-in context) and for checking device rows against oracle rows."""
+import numpy as np
+
+from ccdgpu import abi
+
+
+def rows_from_result(u, cx, cy, width=100):
+    """abi.Unpacked (one chip) -> (row_offsets [n_pix+1], rows ROW_DTYPE): one row per change
+    model, pyccd.default's day-1 row (has_model 0) for a pixel without any; float fields rounded
+    to float32 (Spark's FloatType cast)."""
+    n_pix = u.n_pix
+    counts = np.diff(u.seg_offsets)
+    per = np.maximum(counts, 1)
+    off = np.concatenate([[0], np.cumsum(per)]).astype(np.int64)
+    rows = np.zeros(int(off[-1]), abi.ROW_DTYPE)
+    for p in range(n_pix):
+        r0 = off[p]
+        px, py = cx + 30 * (p % width), cy - 30 * (p // width)
+        a, b = int(u.seg_offsets[p]), int(u.seg_offsets[p + 1])
+        if b == a:
+            rows[r0]['px'], rows[r0]['py'] = px, py
+            rows[r0]['sday'] = rows[r0]['eday'] = rows[r0]['bday'] = 1
+            continue
+        for k, s in enumerate(u.segments[a:b]):
+            r = rows[r0 + k]
+            r['px'], r['py'] = px, py
+            r['sday'], r['eday'], r['bday'] = s['start_day'], s['end_day'], s['break_day']
+            r['curqa'], r['has_model'] = s['curve_qa'], 1
+            r['chprob'] = np.float32(s['change_probability'])
+            r['mag'] = s['magnitude'].astype(np.float32)
+            r['rmse'] = s['rmse'].astype(np.float32)
+            r['intercept'] = s['intercept'].astype(np.float32)
+            r['coef'] = s['coef'].astype(np.float32)
+            rows[r0 + k] = r
+    return off, rows
+
+
+def mask_words(mask, words):
+    """bool [n_pix][n_obs] -> uint32 [n_pix][words] (bit i of word i/32)."""
+    n_pix, n_obs = mask.shape
+    bits = np.zeros((n_pix, words * 32), np.uint8)
+    bits[:, :n_obs] = mask
+    return np.packbits(bits, axis=1, bitorder='little').view('<u4').reshape(n_pix, words)
+
+
+class OracleContext(object):
+    """Stand-in for ccdgpu.Context in CPU tests of the tile runner: the C oracle detects, the
+    rows are restated on the host.  Same slot / fetch protocol as the device context."""
+
+    def __init__(self, device=0, threads=2, delay=0.0):
+        self.device = device
+        self.threads = threads
+        self.delay = delay
+        self.qa_error = False
+        self._slots = {}
+        self._results = None
+
+    def stage_slot_chips(self, slot, batch, params=None):
+        self._slots[slot] = (batch, params)
+
+    def run_slot(self, slot):
+        import time
+        import oracle_ctypes
+        batch, params = self._slots.pop(slot)
+        out = []
+        for c in range(batch.n_chips):
+            d, s, q = batch.chip(c)
+            rc, u = oracle_ctypes.detect_batch(d, s, q, params=params, threads=self.threads)
+            self.qa_error = self.qa_error or rc == abi.E_QA
+            out.append(u)
+        if self.delay:
+            time.sleep(self.delay)
+        self._results = (batch, out)
+
+    def fetch_batch_rows(self, cx, cy, width=100):
+        batch, res = self._results
+        words = (int(batch.n_obs.max()) + 31) // 32
+        offs, rows, bits = [np.zeros(1, np.int64)], [], []
+        for c, u in enumerate(res):
+            o, r = rows_from_result(u, int(cx[c]), int(cy[c]), width)
+            offs.append(o[1:] + offs[-1][-1])
+            rows.append(r)
+            bits.append(mask_words(u.mask, words))
+        return np.concatenate(offs), np.concatenate(rows), np.concatenate(bits)
+
+    def close(self):
+        pass

@@ -1,0 +1,109 @@
+"""The tile driver (ccdc.runner; reference core.changedetection, ccdc/core.py:78-123) on CPU:
+the dynamic chip queue, the two-slot worker pipeline and the gather on rank 0, with the C oracle
+standing in for the device (tests/rows_util.OracleContext).  The world-size-2 gloo run shares
+one queue across two ranks through the process group's store; its gathered per-chip results must
+equal a single-process run's, whatever chip went to which rank."""
+import json
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TILE = os.path.join(ROOT, 'tests', 'golden', 'chipmunk', 'tile_response.json')
+N_PIX = 16
+N_CHIPS = 10
+
+
+def tile():
+    with open(TILE) as f:
+        return json.load(f)
+
+
+def source(pos):
+    import ccdgpu
+    from ccdgpu import synth
+    cfg = synth.config(3)  # base-cadence and sidelap chips (two observation counts)
+    return ccdgpu.ChipBatch.from_chips([synth.chip(cfg, p, 0, N_PIX) for p in pos])
+
+
+def test_tile_fixture_is_the_reference_grid():
+    t = tile()
+    assert len(t['chips']) == 2500 and t['chips'][0] == [t['ulx'], t['uly']]
+
+
+def test_local_queue_hands_out_each_position_once():
+    from ccdc import runner
+    q = runner.LocalQueue(10)
+    got = [q.next(3) for _ in range(5)]
+    assert got == [[0, 1, 2], [3, 4, 5], [6, 7, 8], [9], []]
+
+
+def test_single_process_tile_run():
+    from ccdc import runner
+    from rows_util import OracleContext
+    sink = runner.SummarySink(keep_rows=True)
+    res = runner.changedetection(tile(), source, contexts=2, batch_chips=3, number=N_CHIPS, sink=sink,
+                                 context_factory=lambda dev: OracleContext(dev, threads=2))
+    t = tile()
+    assert res['xys'] == tuple((int(x), int(y)) for x, y in t['chips'][:N_CHIPS])
+    assert [c['pos'] for c in res['chips']] == list(range(N_CHIPS))
+    assert {c['n_obs'] for c in res['chips']} == {1421, 2121}
+    assert sum(st['chips'] for st in res['ranks']) == N_CHIPS
+    # rows of one chip: pixel coordinates from the tile's chip coordinates
+    off, rows, mask = sink.rows[4]
+    cx, cy = (int(v) for v in t['chips'][4])
+    assert rows['px'][off[:-1]].tolist() == [cx + 30 * (p % 100) for p in range(N_PIX)]
+    assert (rows['py'][off[:-1]] == cy).all() and mask.shape == (N_PIX, res['chips'][4]['n_obs'])
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank(rank, world, port, q):
+    sys.path[:0] = [os.path.join(ROOT, 'tests'), os.path.join(ROOT, 'oracle'), os.path.join(ROOT, 'lcmap-firebird_amd')]
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from ccdc import runner
+    from rows_util import OracleContext
+    # rank 1 is slow: the shared queue must hand most chips to rank 0
+    delay = 0.0 if rank == 0 else 4.0
+    res = runner.changedetection(tile(), source, contexts=1, batch_chips=1, number=N_CHIPS,
+                                 context_factory=lambda dev: OracleContext(dev, threads=2, delay=delay))
+    q.put((rank, res))
+    dist.destroy_process_group()
+
+
+def test_tile_run_world2_shares_one_queue_and_gathers_on_rank0():
+    import torch.multiprocessing as mp
+    from ccdc import runner
+    from rows_util import OracleContext
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert out[1] is None  # only rank 0 receives the gather
+    res = out[0]
+    assert [c['pos'] for c in res['chips']] == list(range(N_CHIPS))
+    by_rank = {st['rank']: st['chips'] for st in res['ranks']}
+    assert sum(by_rank.values()) == N_CHIPS and by_rank[0] > by_rank[1] >= 1
+    # same per-chip results as one process detecting the whole tile alone
+    ref = runner.changedetection(tile(), source, contexts=1, batch_chips=4, number=N_CHIPS,
+                                 context_factory=lambda dev: OracleContext(dev, threads=2))
+    assert [c['digest'] for c in res['chips']] == [c['digest'] for c in ref['chips']]
+    assert res['xys'] == ref['xys']
