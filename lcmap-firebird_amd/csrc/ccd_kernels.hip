@@ -112,7 +112,11 @@ static_assert(sizeof(CRow) == 16, "CRow is one dwordx4");
 
 struct Px {
     int n;      // observations (sorted)
-    int m;      // current compacted period length
+    int m;      // current compacted period length (logical rows 0 .. m-1)
+    // Gap buffer: logical row j lives at physical row j (j < gp) or j + gl (j >= gp).  Removing
+    // observations (Tmask, outliers) compacts only the rows between the first removal and the
+    // gap and widens the gap, instead of shifting the whole tail of the period.
+    int gp, gl;
     int peek;   // (adaptive) peek size
     double chg; // change threshold
     const GLOBAL_AS double *basis;
@@ -193,19 +197,28 @@ __device__ __forceinline__ int gidx(const Px &P, int j, int lim, int line) {
     P.bad = ok ? P.bad : line;
     return ok ? j : 0;
 }
-__device__ __forceinline__ int32_t cdr(const Px &P, int j, int line) { return PCD(P)[gidx(P, j, P.m, line)]; }
+// physical row of logical row j (gap buffer)
+__device__ __forceinline__ int ph(const Px &P, int j) { return j + (j >= P.gp ? P.gl : 0); }
+// guarded logical row -> physical row
+__device__ __forceinline__ int prow(const Px &P, int j, int line) { return ph(P, gidx(P, j, P.m, line)); }
+__device__ __forceinline__ int32_t cdr(const Px &P, int j, int line) { return PCD(P)[prow(P, j, line)]; }
 __device__ __forceinline__ int cir(const Px &P, int j, int line) {
-    const int c = PCR(P)[gidx(P, j, P.m, line)].ci;
+    const int c = PCR(P)[prow(P, j, line)].ci;
     return gidx(P, c, P.n, line);
 }
 __device__ __forceinline__ int16_t cvr(const Px &P, int b, int j, int line) {
-    return PCR(P)[gidx(P, j, P.m, line)].v[b];
+    return PCR(P)[prow(P, j, line)].v[b];
 }
 __device__ __forceinline__ CRow crow(const Px &P, int j, int line) {
-    CRow r = PCR(P)[gidx(P, j, P.m, line)];
+    CRow r = PCR(P)[prow(P, j, line)];
     r.ci = (uint16_t)gidx(P, r.ci, P.n, line);
     return r;
 }
+// the 16-byte row of logical row j as one vector load
+__device__ __forceinline__ uint4 crow4(const Px &P, int j, int line) {
+    return reinterpret_cast<const uint4 *>(PCR(P))[prow(P, j, line)];
+}
+#define CROW4(P, j) crow4(P, (j), __LINE__)
 #define CROW(P, j) crow(P, (j), __LINE__)
 #define CDR(P, j) cdr(P, (j), __LINE__)
 #define CIR(P, j) cir(P, (j), __LINE__)
@@ -367,32 +380,41 @@ __device__ __forceinline__ int qabitval(const ccdgpu_params &p, unsigned v) {
 }
 
 // ------------------------------------------------------------------ compaction
-// Drop observations of [a, m) for which drop(j) is true (j = compacted index, valid only for the
-// caller's range); the tail is shifted down in one ascending pass (writes never overtake reads).
+// Drop the observations j in [lo, hi) for which drop(j) is true (logical indices).  Gap buffer:
+// only the logical rows of [min(lo, gp), max(hi, gp)) are rewritten -- the kept ones packed
+// down from physical row min(lo, gp) in one ascending pass -- and the gap moves to the end of
+// that range, widened by the number dropped; rows past the range keep their physical place.
+// The dropped rows leave the processing mask.  Removals happen at the front of the growing
+// window, so the range is a few dozen rows instead of the whole tail of the period.
 template <class F>
-__device__ __forceinline__ int compact_drop(Px &P, int a, F drop) {
+__device__ __forceinline__ int compact_drop(Px &P, int lo, int hi, F drop) {
     const int l = lane();
+    if (lo < P.acc_b) P.acc_a = -1;  // rows of the accumulated Gram window may move
+    hi = hi < P.m ? hi : P.m;
+    const int a = lo < P.gp ? lo : P.gp;
+    const int e = hi > P.gp ? hi : (P.gp < P.m ? P.gp : P.m);
+    PH_COUNT(P, 31, e - a)
     int out = a;
-    if (a < P.acc_b) P.acc_a = -1;  // rows of the accumulated Gram window may move
-    PH_COUNT(P, 31, P.m - a)
-    // four 64-row chunks per round: all their loads go out before the first store (a store lands
-    // at or below its row's old position, so it never overwrites a row still to be read)
+    // four 64-row chunks per round: all their loads go out before the first store (a row's
+    // store lands at or below its own physical position, and physical positions grow with the
+    // logical index, so a store never overwrites a row still to be read)
     constexpr int U = 4;
-    for (int base = a; base < P.m; base += U * W) {
+    for (int base = a; base < e; base += U * W) {
         int32_t d[U];
         uint4 r[U];  // the 16-byte row as one vector (ci = high half of .w)
         bool in[U], dr[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int j = base + u * W + l;
-            in[u] = j < P.m;
+            in[u] = j < e;
             d[u] = 0;
             r[u] = uint4{0u, 0u, 0u, 0u};
             dr[u] = false;
             if (in[u]) {
-                d[u] = PCD(P)[j];
-                r[u] = reinterpret_cast<const uint4 *>(PCR(P))[j];
-                dr[u] = drop(j);
+                const int pj = ph(P, j);
+                d[u] = PCD(P)[pj];
+                r[u] = reinterpret_cast<const uint4 *>(PCR(P))[pj];
+                dr[u] = j >= lo && j < hi && drop(j);
             }
         }
 #pragma unroll
@@ -408,9 +430,12 @@ __device__ __forceinline__ int compact_drop(Px &P, int a, F drop) {
             out += popc(keep);
         }
     }
-    P.m = out;
+    const int removed = (e - a) - (out - a);
+    P.m -= removed;
+    P.gl += removed;
+    P.gp = out;
     psync();
-    return out;
+    return P.m;
 }
 
 // ------------------------------------------------------------------ Lasso (models/lasso.py)
@@ -678,7 +703,7 @@ __device__ __forceinline__ int cd_lanes(Lds *L, int pc, double alpha, int max_it
 
 // residual of band b at compacted observation j for the current models (lasso.predict)
 __device__ __forceinline__ double resid_at(const Px &P, int band, int j) {
-    const int g = gidx(P, j, P.m, __LINE__);
+    const int g = prow(P, j, __LINE__);
     const CRow *rw = PCR(P) + g;  // band value and index read in place (no dynamically indexed copy)
     const GLOBAL_AS double *bs = P.basis + (size_t)gidx(P, rw->ci, P.n, __LINE__) * CCD_BASIS_STRIDE;
     const double *c = LDS().coef[band];
@@ -964,8 +989,8 @@ __device__ __forceinline__ void variogram(Px &P) {
             r1v[u] = uint4{0u, 0u, 0u, 0u};
             if (i < m - kk) {
                 okv[u] = all || (CDR(P, i + kk) - CDR(P, i)) > 30;
-                r0v[u] = reinterpret_cast<const uint4 *>(PCR(P))[i];
-                r1v[u] = reinterpret_cast<const uint4 *>(PCR(P))[i + kk];
+                r0v[u] = CROW4(P, i);
+                r1v[u] = CROW4(P, i + kk);
             }
         }
     };
@@ -1280,7 +1305,7 @@ __device__ __forceinline__ int tmask_reg(Px &P, int a, int b) {
     double x[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
     uint4 q = {0u, 0u, 0u, 0u};  // the observation's row: band values + sorted index
     if (in) {
-        q = reinterpret_cast<const uint4 *>(PCR(P))[gidx(P, a + l, P.m, __LINE__)];
+        q = CROW4(P, a + l);
         const GLOBAL_AS double *bs = P.basis + (size_t)gidx(P, (int)(q.w >> 16), P.n, __LINE__) * CCD_BASIS_STRIDE;
         x[0] = bs[1];
         x[1] = bs[2];
@@ -1596,7 +1621,7 @@ __device__ __forceinline__ bool initialize(Px &P, int &wa, int &wb) {
         if (CDR(P, a + last) - CDR(P, a + first) < p.day_delta || nw - cnt < p.meow_size) { b += 1; continue; }
         if (cnt) {
             const int aa = a, bb = b;
-            compact_drop(P, a, [&](int j) { return j < bb && tflag_at(L, j - aa); });
+            compact_drop(P, a, bb, [&](int j) { return tflag_at(L, j - aa); });
             b -= cnt;
         }
         fit_models(P, a, b, 4);
@@ -1706,7 +1731,7 @@ __device__ __forceinline__ void lookback(Px &P, int &wa, int &wb, int prev) {
         if (m0 > p.outlier_threshold) {
             const int rm = a - 1;
             PH_BEGIN(cp)
-            compact_drop(P, rm, [&](int j) { return j == rm; });
+            compact_drop(P, rm, rm + 1, [&](int j) { return j == rm; });
             PH_END(P, cp, 9)
             a -= 1;
             b -= 1;
@@ -1810,7 +1835,7 @@ __device__ __forceinline__ void build_closest(const Px &P, int fa, int fb, int k
         qn[u] = uint4{0u, 0u, 0u, 0u};
         dn[u] = 0;
         if (i < fb) {
-            qn[u] = reinterpret_cast<const uint4 *>(PCR(P))[gidx(P, i, P.m, __LINE__)];
+            qn[u] = CROW4(P, i);
             dn[u] = CDR(P, i);
         }
     }
@@ -1836,7 +1861,7 @@ __device__ __forceinline__ void build_closest(const Px &P, int fa, int fb, int k
             qn[u] = uint4{0u, 0u, 0u, 0u};
             dn[u] = 0;
             if (i < fb) {
-                qn[u] = reinterpret_cast<const uint4 *>(PCR(P))[gidx(P, i, P.m, __LINE__)];
+                qn[u] = CROW4(P, i);
                 dn[u] = CDR(P, i);
             }
         }
@@ -2353,7 +2378,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
                     }
                     if (m0 > p.outlier_threshold) {
                         const int rm = b;
-                        compact_drop(P, rm, [&](int j) { return j == rm; });
+                        compact_drop(P, rm, rm + 1, [&](int j) { return j == rm; });
                         valid = sp;  // later windows held the removed observation
                         continue;
                     }
@@ -2385,7 +2410,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
             }
             if (m0 > p.outlier_threshold) {
                 const int rm = b;
-                compact_drop(P, rm, [&](int j) { return j == rm; });
+                compact_drop(P, rm, rm + 1, [&](int j) { return j == rm; });
                 continue;
             }
             b += 1;
@@ -2420,7 +2445,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
             }
             if (m0 > p.outlier_threshold) {
                 const int rm = b;
-                compact_drop(P, rm, [&](int j) { return j == rm; });
+                compact_drop(P, rm, rm + 1, [&](int j) { return j == rm; });
                 continue;
             }
             b += 1;
@@ -2542,7 +2567,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
         }
         if (R) {
             PH_BEGIN(cp)
-            compact_drop(P, x0, [&](int j) { return j - x0 < 64 && ((rem >> (j - x0)) & 1ull); });
+            compact_drop(P, x0, x0 + xs, [&](int j) { return ((rem >> (j - x0)) & 1ull) != 0ull; });
             PH_END(P, cp, 9)
         }
         if (change_here) {
@@ -2733,12 +2758,14 @@ __device__ __forceinline__ int px_setup(Px &P, int chip, int pix) {
         }
     }
     P.m = m;
+    P.gp = m;  // no gap yet: logical row = physical row
+    P.gl = 0;
     psync();
     if (proc == CCDGPU_PROC_INSUFFICIENT_CLEAR && m > 0) {
         const CRow *g = PCR(P);
         auto gen = [&](int i, int &val) -> bool { val = (int)g[i].v[1] + 32768; return true; };
         const double med = median_u16(gen, m, m) - 32768.0 + (double)p.median_green_filter;
-        compact_drop(P, 0, [&](int j) { return !((double)g[j].v[1] < med); });
+        compact_drop(P, 0, m, [&](int j) { return !((double)g[j].v[1] < med); });
     }
     return proc;
 }
