@@ -99,13 +99,30 @@ def chip_ids(rank, chips, world=1, n_obs_of=None):
 
 
 def build_batch(cfg, ids, pinned=False):
-    """The chips as one ragged ChipBatch, generated in place (libccdsynth)."""
+    """The chips as one ragged ChipBatch, generated in place (libccdsynth).  With
+    CCD_BENCH_CACHE=<dir> (profiling runs that start the bench several times) the generated
+    buffers are kept there and reloaded instead of regenerated."""
     import ccdgpu
     from ccdgpu import synth
     nobs = [synth.dates(cfg, c).shape[0] for c in ids]
     b = ccdgpu.ChipBatch([PIXELS_PER_CHIP] * len(ids), nobs, pinned=pinned)
+    cache = os.environ.get('CCD_BENCH_CACHE')
+    key = None
+    if cache:
+        import hashlib
+        key = os.path.join(cache, 'batch_%s' % hashlib.sha1(
+            repr((bytes(cfg), list(ids), PIXELS_PER_CHIP)).encode()).hexdigest()[:16])
+        if os.path.exists(key + '.done'):
+            for name in ('dates', 'spectra', 'qa'):
+                getattr(b, name)[...] = np.load('%s_%s.npy' % (key, name), mmap_mode='r')
+            return b
     for j, c in enumerate(ids):
         synth.chip(cfg, c, 0, PIXELS_PER_CHIP, out=b.chip(j))
+    if key:
+        os.makedirs(cache, exist_ok=True)
+        for name in ('dates', 'spectra', 'qa'):
+            np.save('%s_%s.npy' % (key, name), np.asarray(getattr(b, name)))
+        open(key + '.done', 'w').close()
     return b
 
 

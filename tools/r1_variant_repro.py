@@ -16,7 +16,7 @@ import golden_util, parity_util  # noqa: E402
 
 def run(lib_name, variant):
     os.environ['CCDGPU_KERNEL'] = variant
-    L = ctypes.CDLL(os.path.join(ROOT, 'lcmap-firebird_amd', 'lib', lib_name))
+    L = ctypes.CDLL(lib_name if os.path.isabs(lib_name) else os.path.join(ROOT, 'lcmap-firebird_amd', 'lib', lib_name))
     L.ccdgpu_init.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
     L.ccdgpu_detect_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(abi.Params), ctypes.c_int32, ctypes.c_int32,
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(abi.Result)]
@@ -45,9 +45,10 @@ def run(lib_name, variant):
 
 if __name__ == '__main__':
     lib_name = sys.argv[1]
+    variants = sys.argv[2].split(',') if len(sys.argv) > 2 else ['w1', 'w2', 'w3', 'w4']
     base = run(lib_name, 'w3')
     rep = {'lib': lib_name}
-    for v in ('w1', 'w2', 'w3', 'w4'):
+    for v in variants:
         r = base if v == 'w3' else run(lib_name, v)
         rep[v] = {n: {'rc': r[n][0], 'golden_problems': r[n][1], 'identical_to_w3': r[n][2] == base[n][2]} for n in r}
     print(json.dumps(rep))
