@@ -65,6 +65,7 @@ struct __attribute__((aligned(16))) Lds {
     double vario[8];
     double comp[8];        // comparison rmse per band (change_magnitude)
     double med1[8], med2[8];
+    double chg;            // change threshold of the pixel's (adaptive) peek (change.py)
     uint32_t mask[MAXW];   // processing mask, sorted order
     int sel[32];           // compacted indices of the 24 closest-DOY observations
 #ifdef CCD_PHASE_TIMERS
@@ -79,6 +80,10 @@ struct __attribute__((aligned(16))) Lds {
             double tchol[5][5];    // Tmask: Cholesky factor of the unweighted normal matrix
         };
     };
+    // launch statistics of this wave (kept here, not in registers: they are only touched per fit
+    // and at the end): [0] band fits, [1] CD sweeps, [2] counted FP64 flops.  Last member: the
+    // poison test mode fills everything before it.
+    unsigned long long stat[4];
 };
 
 // Launch arguments live in constant memory (uniform scalar loads from every device function),
@@ -97,6 +102,14 @@ __device__ __forceinline__ const CcdDetectArgs &ARGS() {
 }
 extern __shared__ __attribute__((aligned(16))) char ccd_smem[];
 __device__ __forceinline__ Lds &LDS() { return *reinterpret_cast<Lds *>(ccd_smem); }
+// statistics (Lds::stat): a wave-uniform amount added once (lane 0), a per-lane amount from the
+// lanes that carry one
+enum { ST_FITS = 0, ST_SWEEPS = 1, ST_FLOPS = 2 };
+__device__ __forceinline__ int lane();
+__device__ __forceinline__ void stat_uniform(int s, unsigned long long v) {
+    if (lane() == 0) LDS().stat[s] += v;
+}
+__device__ __forceinline__ void stat_lane(int s, unsigned long long v) { atomicAdd(&LDS().stat[s], v); }
 // Peek-residual ring, band-major [band][PSTR observations], aliased with the row staging tile
 // (the Gram staging never overlaps a live ring): lane-contiguous, so lane-per-observation access
 // is bank-conflict free.
@@ -118,7 +131,6 @@ struct Px {
     // gap and widens the gap, instead of shifting the whole tail of the period.
     int gp, gl;
     int peek;   // (adaptive) peek size
-    double chg; // change threshold
     const GLOBAL_AS double *basis;
     const int64_t *sd;
 #ifndef CCD_PERIOD_IN_LDS
@@ -132,9 +144,6 @@ struct Px {
     int acc_a, acc_b;  // window [acc_a, acc_b) whose raw sums L->S holds (acc_a < 0: none)
     int acc_t0;        // date shift of those sums
     int fit_k;         // coefficients of the models in L->coef when they describe [acc_a, acc_b)
-    unsigned long long fits, sweeps;
-    unsigned long long fl;       // counted FP64 flops, wave-uniform part
-    unsigned long long fl_lane;  // counted FP64 flops, per-lane part (coordinate descent)
     mutable int bad;             // source line of a tripped index guard (0 = none), per lane
 };
 
@@ -198,7 +207,14 @@ __device__ __forceinline__ int gidx(const Px &P, int j, int lim, int line) {
     return ok ? j : 0;
 }
 // physical row of logical row j (gap buffer)
-__device__ __forceinline__ int ph(const Px &P, int j) { return j + (j >= P.gp ? P.gl : 0); }
+// (-DCCD_NO_GAP: no gap buffer -- a removal shifts the whole tail, rows never move otherwise)
+__device__ __forceinline__ int ph(const Px &P, int j) {
+#ifdef CCD_NO_GAP
+    return j;
+#else
+    return j + (j >= P.gp ? P.gl : 0);
+#endif
+}
 // guarded logical row -> physical row
 __device__ __forceinline__ int prow(const Px &P, int j, int line) { return ph(P, gidx(P, j, P.m, line)); }
 __device__ __forceinline__ int32_t cdr(const Px &P, int j, int line) { return PCD(P)[prow(P, j, line)]; }
@@ -391,8 +407,13 @@ __device__ __forceinline__ int compact_drop(Px &P, int lo, int hi, F drop) {
     const int l = lane();
     if (lo < P.acc_b) P.acc_a = -1;  // rows of the accumulated Gram window may move
     hi = hi < P.m ? hi : P.m;
+#ifdef CCD_NO_GAP
+    const int a = lo, e = P.m;
+#else
+    if (P.gl == 0) P.gp = lo;  // an empty gap moves for free: start it at the first removal
     const int a = lo < P.gp ? lo : P.gp;
     const int e = hi > P.gp ? hi : (P.gp < P.m ? P.gp : P.m);
+#endif
     PH_COUNT(P, 31, e - a)
     int out = a;
     // four 64-row chunks per round: all their loads go out before the first store (a row's
@@ -432,8 +453,10 @@ __device__ __forceinline__ int compact_drop(Px &P, int lo, int hi, F drop) {
     }
     const int removed = (e - a) - (out - a);
     P.m -= removed;
+#ifndef CCD_NO_GAP
     P.gl += removed;
     P.gp = out;
+#endif
     psync();
     return P.m;
 }
@@ -733,8 +756,8 @@ __device__ __forceinline__ void fit_models(Px &P, int a, int b, int k, bool with
     // coordinate descent: lane = band * 8 + coordinate
     const int sw = cd_lanes(L, pc, p.lasso_alpha * nw, p.lasso_max_iter, p.lasso_tol);
     if ((l & 7) == 0 && (l >> 3) < NB) {
-        P.sweeps += (unsigned long long)sw;  // per-lane; reduced at the end
-        P.fl_lane += (unsigned long long)sw * (unsigned long long)(2 * k * k + 6 * k);  // CD: iters (2k^2 + 6k)
+        stat_lane(ST_SWEEPS, (unsigned long long)sw);
+        stat_lane(ST_FLOPS, (unsigned long long)sw * (unsigned long long)(2 * k * k + 6 * k));  // CD: iters (2k^2 + 6k)
     }
 #ifdef CCD_PHASE_TIMERS
     {
@@ -755,11 +778,11 @@ __device__ __forceinline__ void fit_models(Px &P, int a, int b, int k, bool with
         for (int j = 0; j < 7; ++j) dot += L->xm[j] * L->coef[l][j];
         L->coef[l][7] = L->ym[l] - dot;
     }
-    P.fits += NB;
+    stat_uniform(ST_FITS, NB);
     PH_COUNT(P, 19, 1)
     // SURVEY.md 8(d) op-count model: Gram + column sums n k (k+1), RHS 7 * 2 n k,
     // residual / rmse 7 (2 n k + 3 n)  (k = number of coefficients incl. intercept)
-    P.fl += (unsigned long long)nw * (unsigned long long)(k * (k + 1) + 14 * k + 7 * (2 * k + 3));
+    stat_uniform(ST_FLOPS, (unsigned long long)nw * (unsigned long long)(k * (k + 1) + 14 * k + 7 * (2 * k + 3)));
     wsync();
     PH_END(P, cd, 5)
     PH_BEGIN(rmse)
@@ -1045,7 +1068,7 @@ __device__ __forceinline__ void variogram(Px &P) {
             med = median_u16(gen, cnt, cnt, true);
         }
         if (l == 0) L->vario[band] = med;
-        P.fl += 2ull * (unsigned long long)(m - kk);  // 2 per difference per band
+        stat_uniform(ST_FLOPS, 2ull * (unsigned long long)(m - kk));  // 2 per difference per band
     }
     wsync();
 }
@@ -1053,7 +1076,7 @@ __device__ __forceinline__ void variogram(Px &P) {
 __device__ __forceinline__ void adjust_peek(Px &P) {
     const ccdgpu_params &p = ARGS().p;
     P.peek = p.peek_size;
-    P.chg = p.change_threshold;
+    if (lane() == 0) LDS().chg = p.change_threshold;  // (in LDS: read where compared, never spilled)
     if (!p.adaptive_peek || P.m < 2) return;
     auto gen = [&](int i, int &val) -> bool {
         val = CDR(P, i + 1) - CDR(P, i);
@@ -1069,7 +1092,7 @@ __device__ __forceinline__ void adjust_peek(Px &P) {
         // and finished with the largest supported peek so the launch still drains.
         if (adj > (double)CCDGPU_MAX_PEEK && lane() == 0) atomicMin(&ARGS().counters[7], (unsigned long long)P.gpix);
         P.peek = adj > (double)CCDGPU_MAX_PEEK ? CCDGPU_MAX_PEEK : (int)adj;
-        P.chg = ARGS().thr_table[P.peek];
+        if (lane() == 0) LDS().chg = ARGS().thr_table[P.peek];
     }
 }
 
@@ -1374,7 +1397,7 @@ __device__ __forceinline__ int tmask_reg(Px &P, int a, int b) {
                 tm_solve(Gt, r0, coef);
             }
         }
-        P.fl += (unsigned long long)nw * 35 + 125;  // OLS fit: n_w 35 + 5^3
+        stat_uniform(ST_FLOPS, (unsigned long long)nw * 35 + 125);  // OLS fit: n_w 35 + 5^3
         int iteration = 1;
         bool converged = false;
         while (!converged && iteration < 5) {
@@ -1398,7 +1421,7 @@ __device__ __forceinline__ int tmask_reg(Px &P, int a, int b) {
             tm_normal_reg(x, in ? wt : 0.0, yv, nw, ncol);
             tm_load(L, Gw, rw);
             tm_solve(Gw, rw, coef);
-            P.fl += (unsigned long long)nw * 35 + 125;  // each IRLS refit: n_w 35 + 5^3
+            stat_uniform(ST_FLOPS, (unsigned long long)nw * 35 + 125);  // each IRLS refit: n_w 35 + 5^3
             iteration += 1;
             converged = true;
 #pragma unroll
@@ -1496,7 +1519,7 @@ __device__ __forceinline__ int tmask(Px &P, int a, int b) {
                 tm_solve(Gt, r0, coef);
             }
         }
-        P.fl += (unsigned long long)nw * 35 + 125;  // OLS fit: n_w 35 + 5^3
+        stat_uniform(ST_FLOPS, (unsigned long long)nw * 35 + 125);  // OLS fit: n_w 35 + 5^3
         int iteration = 1;
         bool converged = false;
         while (!converged && iteration < 5) {
@@ -1535,7 +1558,7 @@ __device__ __forceinline__ int tmask(Px &P, int a, int b) {
             tm_normal(P, a, nw, ncol, xoc, xos, band, wt);
             tm_load(&LDS(), Gw, rw);
             tm_solve(Gw, rw, coef);
-            P.fl += (unsigned long long)nw * 35 + 125;  // each IRLS refit: n_w 35 + 5^3
+            stat_uniform(ST_FLOPS, (unsigned long long)nw * 35 + 125);  // each IRLS refit: n_w 35 + 5^3
             iteration += 1;
             converged = true;
 #pragma unroll
@@ -1588,7 +1611,7 @@ __device__ __forceinline__ bool stable(const Px &P, int a, int b) {
         const double v = (fabs(slope) + fabs(resid_at(P, l, a)) + fabs(resid_at(P, l, b - 1))) / rn;
         v2 = v * v;
     }
-    return sqrt(wsum(v2)) < P.chg;
+    return sqrt(wsum(v2)) < LDS().chg;
 }
 __device__ __forceinline__ void count_stable(Px &P) {}
 
@@ -1675,10 +1698,10 @@ __device__ __forceinline__ bool eval_peek(Px &P, int k, int start, int dir, doub
         if (jj < k && bnd < NB) PRES(L)[bnd * PSTR + jj] = r;  // kept for the segment's magnitude medians
         const double v = r / rm;
         const double mag = gsum8((valid && det) ? v * v : 0.0);
-        if (bal(bnd == 0 && jj < k && !(mag > P.chg))) all = false;
+        if (bal(bnd == 0 && jj < k && !(mag > L->chg))) all = false;
         if (pass == 0) mag0 = __shfl(mag, 0);
     }
-    P.fl += (unsigned long long)k * (7 * 2 * 8 + 5 * 3);
+    stat_uniform(ST_FLOPS, (unsigned long long)k * (7 * 2 * 8 + 5 * 3));
     PH_COUNT(P, 18, 1)  // predict 7*2*8 + magnitude 5*3 per peek obs
     wsync();
     return all;
@@ -2309,11 +2332,11 @@ __device__ __forceinline__ void spec_install(Px &P, const SpecFit &F, int s, int
         L->coef[band][7] = F.c;
         L->rmse[band] = F.rmse;
         L->comp[band] = F.rmse;
-        P.sweeps += (unsigned long long)F.sweeps;
-        P.fl_lane += (unsigned long long)F.sweeps * (unsigned long long)(2 * kc * kc + 6 * kc);
+        stat_lane(ST_SWEEPS, (unsigned long long)F.sweeps);
+        stat_lane(ST_FLOPS, (unsigned long long)F.sweeps * (unsigned long long)(2 * kc * kc + 6 * kc));
     }
-    P.fits += NB;
-    P.fl += (unsigned long long)nw * (unsigned long long)(kc * (kc + 1) + 14 * kc + 7 * (2 * kc + 3));
+    stat_uniform(ST_FITS, NB);
+    stat_uniform(ST_FLOPS, (unsigned long long)nw * (unsigned long long)(kc * (kc + 1) + 14 * kc + 7 * (2 * kc + 3)));
     P.fit_k = 0;  // L->coef no longer describes the accumulated Gram window
     PH_COUNT(P, 19, 1)
     wsync();
@@ -2511,28 +2534,20 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
                 irm[t] = t < nd ? 1.0 / rm : 0.0;
             }
             allc = true;
-            // four peek observations per round, their ring reads issued before the first multiply
-            // (rounds past k read other ring entries; their magnitudes are not used)
-            for (int j0 = 0; j0 < k; j0 += 4) {
-                double rv[4][NB];
+            // one peek observation per round: its nd ring reads go out together; a round of four
+            // (28 doubles in flight) pushed the loop's live registers past the budget and the
+            // compiler reloaded the ring address from scratch before every read
+            for (int j = 0; j < k; ++j) {
+                double mg = 0.0;
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-#pragma unroll
-                    for (int t = 0; t < NB; ++t) rv[u][t] = t < nd ? R[bs[t] * PSTR + j0 + u] : 0.0;
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    double mg = 0.0;
-#pragma unroll
-                    for (int t = 0; t < NB; ++t) {
-                        if (t < nd) {
-                            const double v = rv[u][t] * irm[t];
-                            mg += v * v;
-                        }
+                for (int t = 0; t < NB; ++t) {
+                    if (t < nd) {
+                        const double v = R[bs[t] * PSTR + j] * irm[t];
+                        mg += v * v;
                     }
-                    allc = allc && (j0 + u >= k || mg > P.chg);
-                    if (j0 + u == 0) outj = mg > p.outlier_threshold;
                 }
+                allc = allc && mg > L->chg;
+                if (j == 0) outj = mg > p.outlier_threshold;
             }
             PH_END(P, mg, 15)
         }
@@ -2549,8 +2564,8 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
         const bool change_here = Tm && !((TG >> xs) & 1ull);
         // steps executed: 0 .. xs - 1 (plus xs itself when it detects the change)
         const int ne = change_here ? xs + 1 : xs;
-        P.fl += (unsigned long long)ne *
-                ((unsigned long long)k * (7 * 2 * 8 + 5 * 3) + (unsigned long long)nf * 6 + 5 * 48);
+        stat_uniform(ST_FLOPS, (unsigned long long)ne *
+                ((unsigned long long)k * (7 * 2 * 8 + 5 * 3) + (unsigned long long)nf * 6 + 5 * 48));
         PH_COUNT(P, 16, ne)
         PH_COUNT(P, 24, ne <= 16 ? 1 : 0)
         PH_COUNT(P, 25, ne <= 32 ? 1 : 0)
@@ -2600,6 +2615,7 @@ __device__ __forceinline__ void standard_procedure(Px &P) {
     PH_BEGIN(vg)
     variogram(P);
     adjust_peek(P);
+    wsync();  // LDS().chg written by lane 0
     PH_END(P, vg, 2)
     int a = 0, b = meow, prev = 0, nres = 0;
     bool start = true;
@@ -2783,11 +2799,8 @@ __device__ __forceinline__ void detect_body() {
 #endif
     P.fs = as_global(A.s_f64 + (size_t)slot * 8 * nmax);
     P.bk = as_global(A.s_bk + (size_t)slot * nmax);
-    P.fits = 0;
-    P.sweeps = 0;
     P.bad = 0;
-    P.fl = 0;
-    P.fl_lane = 0;
+    if (l < 4) lds.stat[l] = 0ull;
 #ifdef CCD_PHASE_TIMERS
     if (l < CCD_NPHASE) lds.tph[l] = 0;
 #endif
@@ -2821,7 +2834,7 @@ __device__ __forceinline__ void detect_body() {
         if (A.poison) {
             // test mode: no value may come from a previous pixel's (or wave's) LDS contents
             uint4 *w = reinterpret_cast<uint4 *>(&lds);
-            for (int i = l; i < (int)(sizeof(Lds) / 16); i += W) w[i] = uint4{~0u, ~0u, ~0u, ~0u};
+            for (int i = l; i < (int)(offsetof(Lds, stat) / 16); i += W) w[i] = uint4{~0u, ~0u, ~0u, ~0u};
             // ... nor from the slot's global scratch
             for (size_t i = l; i < 8 * nmax; i += W) P.fs[i] = __longlong_as_double(-1ll);
             for (size_t i = l; i < nmax; i += W) P.bk[i] = 0xFFFFu;
@@ -2874,15 +2887,11 @@ __device__ __forceinline__ void detect_body() {
     }
     // instrumentation
     if (l == 0) atomicMax(&A.counters[6], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-    unsigned long long sw = P.sweeps, fll = P.fl_lane;
-    for (int o = 32; o > 0; o >>= 1) {
-        sw += __shfl_xor(sw, o);
-        fll += __shfl_xor(fll, o);
-    }
+    wsync();
     if (l == 0) {
-        atomicAdd(&A.stats[0], P.fits);
-        atomicAdd(&A.stats[1], sw);
-        atomicAdd(&A.stats[2], P.fl + fll);
+        atomicAdd(&A.stats[0], lds.stat[ST_FITS]);
+        atomicAdd(&A.stats[1], lds.stat[ST_SWEEPS]);
+        atomicAdd(&A.stats[2], lds.stat[ST_FLOPS]);
 #ifdef CCD_PHASE_TIMERS
         for (int i = 0; i < CCD_NPHASE; ++i) atomicAdd(&A.stats[8 + i], lds.tph[i]);
 #endif
