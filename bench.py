@@ -59,7 +59,7 @@ def parse():
     ap.add_argument('--contexts', type=int, default=2,
                     help='contexts per GPU running steps concurrently (each stages the same chips)')
     ap.add_argument('--cpu-seconds', type=float, default=12.0, help='target CPU-baseline sample time')
-    ap.add_argument('--restatement-pixels', type=int, default=160,
+    ap.add_argument('--restatement-pixels', type=int, default=1600,
                     help='pixels of the pyccd-structured restatement baseline sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-packer', action='store_true', help='skip the chip-packer (chipmunk decode) leg')
