@@ -68,6 +68,7 @@ def parse():
     ap.add_argument('--no-tile', action='store_true', help='skip the full-tile leg (ccdc.runner over 2500 chips)')
     ap.add_argument('--tile-chips', type=int, default=TILE_CHIPS, help='chips of the tile leg (all ranks together)')
     ap.add_argument('--tile-batch', type=int, default=8, help='chips per launch in the tile leg')
+    ap.add_argument('--tile-contexts', type=int, default=2, help='contexts per GPU in the tile leg')
     ap.add_argument('--share-device', action='store_true',
                     help='rehearsal only: ranks beyond the device count share devices (LOCAL_RANK mod count)')
     return ap.parse_args()
@@ -331,8 +332,8 @@ def tile_leg(args, cfg, rank, world, device, dist):
     if dist is not None:
         dist.barrier()
     t = time.perf_counter()
-    res = runner.changedetection(xys, source, device=device, contexts=2, batch_chips=B, number=args.tile_chips,
-                                 sink=sink)
+    res = runner.changedetection(xys, source, device=device, contexts=args.tile_contexts, batch_chips=B,
+                                 number=args.tile_chips, sink=sink)
     el = time.perf_counter() - t
     if res is None:
         return None
@@ -341,9 +342,10 @@ def tile_leg(args, cfg, rank, world, device, dist):
     for c in res['chips']:
         mix[c['n_obs']] = mix.get(c['n_obs'], 0) + 1
     return {'value': px / el, 'unit': 'pixels/s', 'seconds': el, 'chips': len(res['chips']), 'pixels': px,
-            'chips_per_launch': B, 'contexts_per_gpu': 2, 'ranks': world, 'n_obs_mix': mix,
+            'chips_per_launch': B, 'contexts_per_gpu': args.tile_contexts, 'ranks': world, 'n_obs_mix': mix,
             'rows': sum(c['rows'] for c in res['chips']),
             'chips_per_rank': {st['rank']: st['chips'] for st in res['ranks']},
+            'worker_seconds_rank0': {k: round(v, 3) for k, v in res['ranks'][0].items() if k.endswith('_seconds')},
             'note': 'ccdc.runner tile driver: shared dynamic chip queue, H2D of pinned ARD + detection + device row packing + D2H of rows + gather of per-chip summaries on rank 0; chip ARD cycled over 2 pre-generated pinned batches of the tile mix'}
 
 

@@ -131,38 +131,50 @@ def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, er
     try:
         pending = None
         slot = 0
+        clock = time.perf_counter
         while True:
+            t0 = clock()
             pos = queue.next(batch_chips)
             nxt = None
             if pos:
                 batch = source(pos)
                 if batch.n_chips != len(pos):
                     raise ValueError('source returned %d chips for %d positions' % (batch.n_chips, len(pos)))
+                t1 = clock()
                 ctx.stage_slot_chips(slot, batch, params)
                 nxt = (slot, pos, batch)
                 slot ^= 1
+            else:
+                t1 = clock()
+            t2 = clock()
             if pending is not None:
                 s, ppos, pbatch = pending
-                t0 = time.perf_counter()
                 ctx.run_slot(s)
                 if getattr(ctx, 'qa_error', False):
                     import ccdgpu
                     raise ccdgpu.QAValueError('unsupported bit-packed QA value in chips at tile positions %s' % (ppos,))
+                t3 = clock()
                 cx = np.array([xys[p][0] for p in ppos], dtype=np.int32)
                 cy = np.array([xys[p][1] for p in ppos], dtype=np.int32)
                 off, rows, mask = ctx.fetch_batch_rows(cx, cy, width)
-                t1 = time.perf_counter()
+                t4 = clock()
                 for c, p in enumerate(ppos):
                     p0, p1 = int(pbatch.pix_off[c]), int(pbatch.pix_off[c + 1])
                     r0, r1 = int(off[p0]), int(off[p1])
                     d, _, _ = pbatch.chip(c)
                     sink(p, int(cx[c]), int(cy[c]), d, off[p0:p1 + 1] - r0, rows[r0:r1], pbatch.mask_bits_of(mask, c))
+                t5 = clock()
                 with stats['lock']:
                     stats['batches'] += 1
                     stats['chips'] += len(ppos)
                     stats['pixels'] += pbatch.total_pixels
                     stats['rows'] += int(rows.shape[0])
-                    stats['device_seconds'] += t1 - t0
+                    stats['device_seconds'] += t3 - t2
+                    stats['fetch_seconds'] += t4 - t3
+                    stats['sink_seconds'] += t5 - t4
+            with stats['lock']:
+                stats['source_seconds'] += t1 - t0
+                stats['stage_seconds'] += t2 - t1
             pending = nxt
             if pending is None:
                 break
@@ -184,7 +196,10 @@ def detect_tile(xys, source, queue, device=0, contexts=2, batch_chips=16, params
         import ccdgpu
         context_factory = ccdgpu.Context
     sink = sink if sink is not None else SummarySink()
-    stats = {'lock': threading.Lock(), 'batches': 0, 'chips': 0, 'pixels': 0, 'rows': 0, 'device_seconds': 0.0}
+    # per-phase host seconds summed over the workers: source (ARD fetch), stage (upload call),
+    # device (run_slot: waits for the upload, detects), fetch (row packing + D2H), sink
+    stats = {'lock': threading.Lock(), 'batches': 0, 'chips': 0, 'pixels': 0, 'rows': 0, 'device_seconds': 0.0,
+             'source_seconds': 0.0, 'stage_seconds': 0.0, 'fetch_seconds': 0.0, 'sink_seconds': 0.0}
     errors = []
     ctxs = [context_factory(device) for _ in range(max(1, int(contexts)))]
     t0 = time.perf_counter()
