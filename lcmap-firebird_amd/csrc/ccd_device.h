@@ -27,6 +27,10 @@
 #define CCD_NB 7
 #define CCD_WAVE 64
 #define CCD_BASIS_STRIDE 8
+// per-slot double scratch: [8][n_obs_max] (Tmask columns / closest-DOY r^2) + the overflow of
+// the peek-residual ring (7 bands x (CCDGPU_MAX_PEEK - 64) observations)
+#define CCD_RING_OVF 256
+#define CCD_SLOT_F64(nmax) ((size_t)8 * (size_t)(nmax) + CCD_RING_OVF)
 // launch-argument slots in constant memory: contexts of one process that can run at once
 #define CCD_ARG_SLOTS 16
 
@@ -55,7 +59,7 @@ struct CcdDetectArgs {
     // per-slot scratch
     int32_t *s_date;
     uint16_t *s_row;  // [n_slots][n_obs][8]: int16 band values 0..6, uint16 sorted index
-    double *s_f64;   // [n_slots][8][n_obs] Tmask scratch / closest-DOY squared residuals
+    double *s_f64;   // [n_slots][CCD_SLOT_F64(n_obs)] Tmask scratch / closest-DOY squared residuals / ring overflow
     uint16_t *s_bk;  // [n_slots][n_obs] closest-DOY bucket list
     // outputs
     uint32_t *mask_bits;

@@ -39,10 +39,13 @@ constexpr int W = CCD_WAVE;
 constexpr int RW = 16;  // doubles per staged design row: t c1 s1 c2 s2 c3 s3 _ y0..y6 _
 constexpr int TR = 32;  // rows per LDS staging tile
 constexpr int MAXW = CCDGPU_MAX_OBS / 32;
-constexpr int PSTR = CCDGPU_MAX_PEEK;  // band stride of the peek-residual ring
+constexpr int PSTR = CCD_WAVE;  // band stride of the LDS peek-residual ring (a batch's 64 rows)
+// Peek observations past the ring's 64 (an adaptive peek of 65 .. CCDGPU_MAX_PEEK, evaluated one
+// step at a time) keep their residuals in the slot's global scratch, after its [8][n] block.
+constexpr int POVF = CCDGPU_MAX_PEEK - PSTR;
+static_assert(NB * POVF <= CCD_RING_OVF, "ring overflow fits the slot scratch tail");
 #define CCD_NPHASE (CCD_NSTATS - 8)
 
-static_assert(PSTR >= CCD_WAVE, "the ring holds a lookforward batch's 64 rows per band");
 // Global-memory pointers kept in the per-pixel state are typed address_space(1) so every access
 // is a global_* instruction (a generic pointer would compile to flat_*, which also counts against
 // lgkmcnt and makes every later LDS wait wait for the global load too).
@@ -66,7 +69,6 @@ struct __attribute__((aligned(16))) Lds {
     double comp[8];        // comparison rmse per band (change_magnitude)
     double med1[8], med2[8];
     double chg;            // change threshold of the pixel's (adaptive) peek (change.py)
-    uint32_t mask[MAXW];   // processing mask, sorted order
     int sel[32];           // compacted indices of the 24 closest-DOY observations
 #ifdef CCD_PHASE_TIMERS
     unsigned long long tph[CCD_NPHASE];  // diagnostic build: per-phase cycle totals of this wave
@@ -85,6 +87,10 @@ struct __attribute__((aligned(16))) Lds {
     // poison test mode fills everything before it.
     unsigned long long stat[4];
 };
+#ifndef CCD_PHASE_TIMERS
+// <= 10 KB: 16 waves per CU fit in the 160 KB LDS (the 128-VGPR variant's register occupancy)
+static_assert(sizeof(Lds) <= 10240, "per-wave LDS block within 160 KB / 16 waves");
+#endif
 
 // Launch arguments live in constant memory (uniform scalar loads from every device function),
 // one slot per host context so that contexts sharing a device can run concurrently; the launch
@@ -146,6 +152,13 @@ struct Px {
     int fit_k;         // coefficients of the models in L->coef when they describe [acc_a, acc_b)
     mutable int bad;             // source line of a tripped index guard (0 = none), per lane
 };
+// the pixel's processing mask: its output words, updated in place (Tmask / outlier removals)
+__device__ __forceinline__ GLOBAL_AS unsigned *pmask(const Px &P) {
+    return as_global(ARGS().mask_bits) + (size_t)P.gpix * ARGS().mask_words;
+}
+// peek residuals of observations 64 .. CCDGPU_MAX_PEEK-1, band-major [band][POVF], after the
+// slot's [8][n] double scratch
+__device__ __forceinline__ GLOBAL_AS double *ring_ovf(const Px &P) { return P.fs + (size_t)8 * ARGS().n_obs_max; }
 
 // Where the compacted period lives.  CCD_PERIOD_IN_LDS: in the wave's LDS block right after the
 // Lds struct (dates, then rows at a 16-byte aligned offset) -- every period access is a ds_*
@@ -442,7 +455,8 @@ __device__ __forceinline__ int compact_drop(Px &P, int lo, int hi, F drop) {
         for (int u = 0; u < U; ++u) {
             const unsigned long long keep = bal(in[u] && !dr[u]);
             const unsigned ci = r[u].w >> 16;
-            if (in[u] && dr[u]) atomicAnd(&LDS().mask[ci >> 5], ~(1u << (ci & 31)));
+            if (in[u] && dr[u])
+                __hip_atomic_fetch_and(pmask(P) + (ci >> 5), ~(1u << (ci & 31)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (in[u] && !dr[u]) {
                 const int pos = gidx(P, out + below(keep), P.n, __LINE__);
                 PCD(P)[pos] = d[u];
@@ -1688,14 +1702,17 @@ __device__ __forceinline__ bool eval_peek(Px &P, int k, int start, int dir, doub
         rr[pass] = (pass * 8 < k && jj < k && bnd < NB) ? resid_at(P, bnd, start + dir * jj) : 0.0;
     }
 #pragma unroll
-    for (int pass = 0; pass < PSTR / 8; ++pass) {
+    for (int pass = 0; pass < CCDGPU_MAX_PEEK / 8; ++pass) {
         if (pass * 8 >= k) break;
         const int jj = pass * 8 + osub;
         const bool valid = jj < k && bnd < NB;
         double r = 0.0;
         if (pass < 4) r = rr[pass < 4 ? pass : 0];
         else if (valid) r = resid_at(P, bnd, start + dir * jj);
-        if (jj < k && bnd < NB) PRES(L)[bnd * PSTR + jj] = r;  // kept for the segment's magnitude medians
+        if (jj < k && bnd < NB) {  // kept for the segment's magnitude medians
+            if (pass < PSTR / 8) PRES(L)[bnd * PSTR + jj] = r;
+            else ring_ovf(P)[bnd * POVF + jj - PSTR] = r;
+        }
         const double v = r / rm;
         const double mag = gsum8((valid && det) ? v * v : 0.0);
         if (bal(bnd == 0 && jj < k && !(mag > L->chg))) all = false;
@@ -1716,12 +1733,19 @@ __device__ __forceinline__ double peek_medians(Px &P, int k, int off) {
     const int bnd = l & 7, osub = l >> 3;
     const int t1 = (k - 1) / 2, t2 = k / 2;
     const double *R = PRES(L) + bnd * PSTR + off;
+    // observations past the LDS ring (k > 64: off is 0 then) are in the global overflow
+    const int kl = k < PSTR - off ? k : PSTR - off;
+    const GLOBAL_AS double *Ro = ring_ovf(P) + bnd * POVF - PSTR;
     for (int jj = osub; jj < k; jj += 8) {
         if (bnd >= NB) continue;
-        const double v = R[jj];
+        const double v = jj < kl ? R[jj] : Ro[jj];
         int rank = 0;
-        for (int i = 0; i < k; ++i) {
+        for (int i = 0; i < kl; ++i) {
             const double u = R[i];
+            rank += (u < v || (u == v && i < jj)) ? 1 : 0;
+        }
+        for (int i = kl; i < k; ++i) {
+            const double u = Ro[i];
             rank += (u < v || (u == v && i < jj)) ? 1 : 0;
         }
         if (rank == t1) L->med1[bnd] = v;
@@ -2643,7 +2667,6 @@ __device__ __forceinline__ void standard_procedure(Px &P) {
 __device__ __forceinline__ int px_setup(Px &P, int chip, int pix) {
     const CcdDetectArgs &A = ARGS();
     const ccdgpu_params &p = A.p;
-    Lds *L = &LDS();
     const int l = lane();
     const int n = P.n;
     const int64_t data_off = A.chip_data_off[chip];
@@ -2700,7 +2723,10 @@ __device__ __forceinline__ int px_setup(Px &P, int chip, int pix) {
     else
         proc = CCDGPU_PROC_STANDARD;
     const bool conv = proc == CCDGPU_PROC_STANDARD && p.kelvin_to_celsius;
-    for (int i = l; i < A.mask_words; i += W) L->mask[i] = 0u;
+    // processing mask: written straight into the pixel's output words (words past the chip's own
+    // n are zero; the chunk loop below writes the rest)
+    GLOBAL_AS unsigned *mk = pmask(P);
+    for (int i = ((n + 31) >> 5) + l; i < A.mask_words; i += W) mk[i] = 0u;
     int m = 0;
     int carry = -1;  // date of the last kept observation (ordinals are >= 1)
     constexpr int U2 = 2;  // two chunks per round: their gathers (order -> qa, 7 bands, date) together,
@@ -2767,8 +2793,8 @@ __device__ __forceinline__ int px_setup(Px &P, int chip, int pix) {
             PCR(P)[pos] = cw;
         }
         if (l == 0 && base < n) {
-            L->mask[base >> 5] = (unsigned)k2;
-            if (base + 32 < n) L->mask[(base >> 5) + 1] = (unsigned)(k2 >> 32);
+            mk[base >> 5] = (unsigned)k2;
+            if (base + 32 < n) mk[(base >> 5) + 1] = (unsigned)(k2 >> 32);
         }
         m += popc(k2);
         }
@@ -2797,7 +2823,7 @@ __device__ __forceinline__ void detect_body() {
     P.cd = A.s_date + (size_t)slot * nmax;
     P.cr = reinterpret_cast<CRow *>(A.s_row) + (size_t)slot * nmax;
 #endif
-    P.fs = as_global(A.s_f64 + (size_t)slot * 8 * nmax);
+    P.fs = as_global(A.s_f64 + (size_t)slot * CCD_SLOT_F64(nmax));
     P.bk = as_global(A.s_bk + (size_t)slot * nmax);
     P.bad = 0;
     if (l < 4) lds.stat[l] = 0ull;
@@ -2836,7 +2862,7 @@ __device__ __forceinline__ void detect_body() {
             uint4 *w = reinterpret_cast<uint4 *>(&lds);
             for (int i = l; i < (int)(offsetof(Lds, stat) / 16); i += W) w[i] = uint4{~0u, ~0u, ~0u, ~0u};
             // ... nor from the slot's global scratch
-            for (size_t i = l; i < 8 * nmax; i += W) P.fs[i] = __longlong_as_double(-1ll);
+            for (size_t i = l; i < CCD_SLOT_F64(nmax); i += W) P.fs[i] = __longlong_as_double(-1ll);
             for (size_t i = l; i < nmax; i += W) P.bk[i] = 0xFFFFu;
 #ifndef CCD_PERIOD_IN_LDS
             for (size_t i = l; i < nmax; i += W) {
@@ -2869,7 +2895,6 @@ __device__ __forceinline__ void detect_body() {
         }
         wsync();
         PH_END(P, tot, 0)
-        for (int i = l; i < A.mask_words; i += W) A.mask_bits[(size_t)job * A.mask_words + i] = lds.mask[i];
         if (l == 0) {
             A.procedure[job] = proc;
             A.nseg[job] = P.nseg;

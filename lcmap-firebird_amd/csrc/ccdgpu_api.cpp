@@ -385,7 +385,7 @@ static int stage_alloc(ccdgpu_ctx *c, const ccdgpu_params *params, const Shape &
     const size_t ns = (size_t)c->n_slots, no = (size_t)sh.n_obs_max;
     const size_t nper = ccdk_period_in_lds() ? 1 : ns * no;  // global period scratch only when not in LDS
     if ((rc = c->s_date.ensure(nper)) || (rc = c->s_row.ensure(nper * 8)) ||
-        (rc = c->s_f64.ensure(ns * 8 * no)) || (rc = c->s_bk.ensure(ns * no)))
+        (rc = c->s_f64.ensure(ns * CCD_SLOT_F64(no))) || (rc = c->s_bk.ensure(ns * no)))
         return rc;
     if (c->pool_cap < c->total_pix * 8) c->pool_cap = c->total_pix * 8;
     if ((rc = c->pool.ensure(c->pool_cap)) || (rc = c->pool_seq.ensure(c->pool_cap))) return rc;
