@@ -2514,14 +2514,25 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
         ring_rows(P, x0);
         PH_END(P, rr, 13)
         PH_COUNT(P, 17, 1)
-        const bool valid = l < B && x0 + l + k < m0;
-        const unsigned long long V = bal(valid);
+        bool valid = l < B && x0 + l + k < m0;
         const int da = CDR(P, a);
         const int dprev = CDR(P, x0 - 1);
-        int dj = 0;
+        const int dj = valid ? CDR(P, x0 + l) : 0;
+        {
+            // Steps past the first span-test refit are never executed.  Without removals step l's
+            // last kept observation is x0 + l - 1; a removal only moves it earlier (the refit
+            // later), so the first such step under that assumption bounds the batch from below:
+            // lanes more than 2 steps past it are left out (with more removals before it the batch
+            // ends there without a terminal step and the next one continues).
+            const int dp = __shfl(dj, l > 0 ? l - 1 : 0);
+            const bool t0 = valid && ((double)(l > 0 ? dp : dprev) - (double)da) >= 1.33 * fit_span;
+            const unsigned long long T0 = bal(t0);
+            const int lim = T0 ? __ffsll((long long)T0) + 1 : W;  // first such step + 2
+            valid = valid && l <= lim;
+        }
+        const unsigned long long V = bal(valid);
         bool allc = false, outj = false;
         if (valid) {
-            dj = CDR(P, x0 + l);
             // comparison rmse per detection band: cs[s] for the s-th detection band bs[s]
             const unsigned dm = det_mask();
             const int nd = __builtin_popcount(dm);
@@ -2546,7 +2557,6 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
             }
             PH_END(P, cmp, 14)
             PH_BEGIN(mg)
-            const double *R = PRES(L) + l;
             // change_magnitude: (r / max(vario, comp))^2 summed over the detection bands (in band
             // order), with the division as a multiply by the band's reciprocal (one division per
             // band and step)
@@ -2558,17 +2568,21 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
                 irm[t] = t < nd ? 1.0 / rm : 0.0;
             }
             allc = true;
-            // one peek observation per round: its nd ring reads go out together; a round of four
-            // (28 doubles in flight) pushed the loop's live registers past the budget and the
-            // compiler reloaded the ring address from scratch before every read
+            // One peek observation per round: its 7 ring reads go out together (a band past the
+            // detection bands reads band 0's row and adds 0: irm is 0 there, ring rows are
+            // finite).  The lane's ring address is re-derived every round (lane() is opaque), so
+            // no per-lane address stays live across the loop for the allocator to spill -- a
+            // spilled one cost a scratch reload and a full wait before every read.
             for (int j = 0; j < k; ++j) {
+                const double *Rj = PRES(L) + lane() + j;
+                double rv[NB];
+#pragma unroll
+                for (int t = 0; t < NB; ++t) rv[t] = Rj[bs[t] * PSTR];
                 double mg = 0.0;
 #pragma unroll
                 for (int t = 0; t < NB; ++t) {
-                    if (t < nd) {
-                        const double v = R[bs[t] * PSTR + j] * irm[t];
-                        mg += v * v;
-                    }
+                    const double v = rv[t] * irm[t];
+                    mg += v * v;
                 }
                 allc = allc && mg > L->chg;
                 if (j == 0) outj = mg > p.outlier_threshold;
