@@ -678,6 +678,7 @@ __device__ __forceinline__ int cd_sweep(Lds *L, int pc_rt, double alpha, int max
     const double q = act ? L->Q[k][b] : 0.0;
     const double yy = b < NB ? L->YY[b] : 0.0;
     const double tol_s = tol * yy;
+    const double tol_m = -0x1p-45 * tol;  // exact (a power of two)
     const bool can = act && gkk != 0.0;  // sklearn skips zero-norm columns
     double w = 0.0, g = q;
     bool done = b >= NB;
@@ -696,9 +697,14 @@ __device__ __forceinline__ int cd_sweep(Lds *L, int pc_rt, double alpha, int max
         // every coordinate moves once per sweep: d_w_ii = |w_new - w_old| of the lane's own one
         const double d_w_max = gmax8(fabs(w - w0));
         const double w_max = gmax8(fabs(w));  // w stays 0 in lanes outside the model
-        // sklearn's d_w_max / w_max < tol, as one branch-free division (w_max = 0 is the check's
-        // own first clause)
-        const bool ratio_lt = d_w_max / w_max < tol;
+        // sklearn's d_w_max / w_max < tol (w_max = 0 is the check's own first clause).  The sign
+        // of the fused d_w_max - tol w_max (one rounding of the exact value) decides it outside a
+        // sliver of relative width 2^-45 around tol, where the quotient itself is taken:
+        // r >= 0 -> d/w >= tol -> fl(d/w) >= tol; r < -2^-45 tol w -> fl(d/w) < tol.
+        const double r = fma(-tol, w_max, d_w_max);
+        bool ratio_lt = r < tol_m * w_max;
+        const bool amb = !(r >= 0.0) && !ratio_lt;
+        if (bal(amb)) ratio_lt = amb ? d_w_max / w_max < tol : ratio_lt;
         const bool check = !done && (w_max == 0.0 || ratio_lt || it == max_iter - 1);
         if (bal(check)) {
             const double xta = act ? g : 0.0;  // X^T R
