@@ -69,6 +69,7 @@ def parse():
     ap.add_argument('--tile-chips', type=int, default=TILE_CHIPS, help='chips of the tile leg (all ranks together)')
     ap.add_argument('--tile-batch', type=int, default=8, help='chips per launch in the tile leg')
     ap.add_argument('--tile-contexts', type=int, default=2, help='contexts per GPU in the tile leg')
+    ap.add_argument('--tile-depth', type=int, default=2, help='batches each tile-leg context keeps uploaded ahead')
     ap.add_argument('--share-device', action='store_true',
                     help='rehearsal only: ranks beyond the device count share devices (LOCAL_RANK mod count)')
     return ap.parse_args()
@@ -308,8 +309,8 @@ def main():
 def tile_leg(args, cfg, rank, world, device, dist):
     """The product tile driver (ccdc.runner.changedetection; reference core.changedetection,
     ccdc/core.py:78-123) over the tile's chip grid on every rank's GPU: one dynamic chip queue
-    shared by all ranks (the process group's store), two contexts per GPU each double-buffering
-    pinned uploads, detection, device row packing, rows fetched back per batch, per-chip
+    shared by all ranks (the process group's store), two contexts per GPU each keeping two pinned
+    batch uploads queued ahead of its detection, device row packing, rows fetched back per batch, per-chip
     summaries gathered on rank 0.  PCIe-inclusive.  Chip ARD comes from a pool of two
     pre-generated pinned batches of the tile's cadence mix, cycled over the tile positions, so
     host-side synthetic generation (the chipmunk fetch stand-in) stays out of the timing."""
@@ -333,7 +334,7 @@ def tile_leg(args, cfg, rank, world, device, dist):
         dist.barrier()
     t = time.perf_counter()
     res = runner.changedetection(xys, source, device=device, contexts=args.tile_contexts, batch_chips=B,
-                                 number=args.tile_chips, sink=sink)
+                                 number=args.tile_chips, sink=sink, upload_depth=args.tile_depth)
     el = time.perf_counter() - t
     if res is None:
         return None
@@ -342,7 +343,8 @@ def tile_leg(args, cfg, rank, world, device, dist):
     for c in res['chips']:
         mix[c['n_obs']] = mix.get(c['n_obs'], 0) + 1
     return {'value': px / el, 'unit': 'pixels/s', 'seconds': el, 'chips': len(res['chips']), 'pixels': px,
-            'chips_per_launch': B, 'contexts_per_gpu': args.tile_contexts, 'ranks': world, 'n_obs_mix': mix,
+            'chips_per_launch': B, 'contexts_per_gpu': args.tile_contexts, 'upload_depth': args.tile_depth,
+            'ranks': world, 'n_obs_mix': mix,
             'rows': sum(c['rows'] for c in res['chips']),
             'chips_per_rank': {st['rank']: st['chips'] for st in res['ranks']},
             'worker_seconds_rank0': {k: round(v, 3) for k, v in res['ranks'][0].items() if k.endswith('_seconds')},

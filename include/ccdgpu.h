@@ -185,13 +185,16 @@ int ccdgpu_stage_chipmunk(ccdgpu_ctx *ctx, const ccdgpu_params *params, int32_t 
                           int32_t n_obs, const int64_t *dates, const char *text, int64_t text_bytes,
                           const int64_t *text_offsets, double *unpack_seconds);
 
-/* Overlapped upload (HIP copy stream): ccdgpu_stage_slot uploads a batch into input slot 0 or
- * 1 and returns at once; ccdgpu_run_slot detects the batch of a slot (after its upload) exactly
- * like ccdgpu_run_staged, results fetched with ccdgpu_fetch_staged / ccdgpu_fetch_rows.  The
- * streaming loop  stage_slot(0, b0); for i: { stage_slot((i+1)&1, b_{i+1}); run_slot(i&1); fetch }
- * overlaps each upload with the previous batch's detection.  Host inputs must stay valid and
+/* Overlapped upload (HIP copy stream): ccdgpu_stage_slot uploads a batch into input slot
+ * 0 .. CCDGPU_UPLOAD_SLOTS-1 and returns at once; ccdgpu_run_slot detects the batch of a slot
+ * (after its upload) exactly like ccdgpu_run_staged, results fetched with ccdgpu_fetch_staged /
+ * ccdgpu_fetch_rows.  The streaming loop  stage_slot(0, b0); for i: { stage_slot((i+1)&1,
+ * b_{i+1}); run_slot(i&1); fetch }  overlaps each upload with the previous batch's detection;
+ * with S slots up to S-1 uploads can be queued ahead of the running batch (the tile driver keeps
+ * two queued, so the PCIe link stays busy while detection and the row fetch run).  Host inputs must stay valid and
  * unchanged until the run_slot of their slot returns; they should be pinned (ccdgpu_host_alloc),
  * or the upload is synchronous.  Each slot keeps the params it was staged with. */
+#define CCDGPU_UPLOAD_SLOTS 4
 int ccdgpu_host_alloc(size_t bytes, void **ptr);
 int ccdgpu_host_free(void *ptr);
 int ccdgpu_stage_slot_chips(ccdgpu_ctx *ctx, int32_t slot, const ccdgpu_params *params, int32_t n_chips,

@@ -126,64 +126,68 @@ class ParquetSink(object):
 
 
 # --------------------------------------------------------------------------- the GPU worker
-def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, errors):
-    """One context: double-buffered upload slots, so batch i+1 uploads while batch i runs."""
+def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, errors, depth=2):
+    """One context: up to ``depth`` batches uploaded (or uploading) ahead of the one being
+    detected, one upload slot each, so the PCIe link stays busy while a batch is detected and
+    its rows are fetched (with one batch ahead the link idles whenever both of a GPU's contexts
+    are past their upload)."""
     try:
-        pending = None
-        slot = 0
         clock = time.perf_counter
+        free = list(range(depth + 1))
+        staged = []  # (slot, positions, batch), in upload order
+        exhausted = False
         while True:
-            t0 = clock()
-            pos = queue.next(batch_chips)
-            nxt = None
-            if pos:
+            while free and not exhausted:
+                t0 = clock()
+                pos = queue.next(batch_chips)
+                if not pos:
+                    exhausted = True
+                    break
                 batch = source(pos)
                 if batch.n_chips != len(pos):
                     raise ValueError('source returned %d chips for %d positions' % (batch.n_chips, len(pos)))
                 t1 = clock()
+                slot = free.pop(0)
                 ctx.stage_slot_chips(slot, batch, params)
-                nxt = (slot, pos, batch)
-                slot ^= 1
-            else:
-                t1 = clock()
-            t2 = clock()
-            if pending is not None:
-                s, ppos, pbatch = pending
-                ctx.run_slot(s)
-                if getattr(ctx, 'qa_error', False):
-                    import ccdgpu
-                    raise ccdgpu.QAValueError('unsupported bit-packed QA value in chips at tile positions %s' % (ppos,))
-                t3 = clock()
-                cx = np.array([xys[p][0] for p in ppos], dtype=np.int32)
-                cy = np.array([xys[p][1] for p in ppos], dtype=np.int32)
-                off, rows, mask = ctx.fetch_batch_rows(cx, cy, width)
-                t4 = clock()
-                for c, p in enumerate(ppos):
-                    p0, p1 = int(pbatch.pix_off[c]), int(pbatch.pix_off[c + 1])
-                    r0, r1 = int(off[p0]), int(off[p1])
-                    d, _, _ = pbatch.chip(c)
-                    sink(p, int(cx[c]), int(cy[c]), d, off[p0:p1 + 1] - r0, rows[r0:r1], pbatch.mask_bits_of(mask, c))
-                t5 = clock()
+                staged.append((slot, pos, batch))
+                t2 = clock()
                 with stats['lock']:
-                    stats['batches'] += 1
-                    stats['chips'] += len(ppos)
-                    stats['pixels'] += pbatch.total_pixels
-                    stats['rows'] += int(rows.shape[0])
-                    stats['device_seconds'] += t3 - t2
-                    stats['fetch_seconds'] += t4 - t3
-                    stats['sink_seconds'] += t5 - t4
-            with stats['lock']:
-                stats['source_seconds'] += t1 - t0
-                stats['stage_seconds'] += t2 - t1
-            pending = nxt
-            if pending is None:
+                    stats['source_seconds'] += t1 - t0
+                    stats['stage_seconds'] += t2 - t1
+            if not staged:
                 break
+            s, ppos, pbatch = staged.pop(0)
+            t2 = clock()
+            ctx.run_slot(s)
+            if getattr(ctx, 'qa_error', False):
+                import ccdgpu
+                raise ccdgpu.QAValueError('unsupported bit-packed QA value in chips at tile positions %s' % (ppos,))
+            t3 = clock()
+            cx = np.array([xys[p][0] for p in ppos], dtype=np.int32)
+            cy = np.array([xys[p][1] for p in ppos], dtype=np.int32)
+            off, rows, mask = ctx.fetch_batch_rows(cx, cy, width)
+            free.append(s)  # its rows are fetched: the slot takes the next upload
+            t4 = clock()
+            for c, p in enumerate(ppos):
+                p0, p1 = int(pbatch.pix_off[c]), int(pbatch.pix_off[c + 1])
+                r0, r1 = int(off[p0]), int(off[p1])
+                d, _, _ = pbatch.chip(c)
+                sink(p, int(cx[c]), int(cy[c]), d, off[p0:p1 + 1] - r0, rows[r0:r1], pbatch.mask_bits_of(mask, c))
+            t5 = clock()
+            with stats['lock']:
+                stats['batches'] += 1
+                stats['chips'] += len(ppos)
+                stats['pixels'] += pbatch.total_pixels
+                stats['rows'] += int(rows.shape[0])
+                stats['device_seconds'] += t3 - t2
+                stats['fetch_seconds'] += t4 - t3
+                stats['sink_seconds'] += t5 - t4
     except BaseException as e:  # reported by detect_tile after the other workers drain
         errors.append(e)
 
 
 def detect_tile(xys, source, queue, device=0, contexts=2, batch_chips=16, params=None, width=100,
-                sink=None, context_factory=None):
+                sink=None, context_factory=None, upload_depth=2):
     """Change detection of the tile chips at ``xys`` (list of (cx, cy), tile order) on one GPU.
 
     ``source(positions) -> ccdgpu.ChipBatch`` supplies the ARD of the chips at those tile
@@ -191,7 +195,8 @@ def detect_tile(xys, source, queue, device=0, contexts=2, batch_chips=16, params
     for one process, StoreQueue across ranks); ``sink(pos, cx, cy, dates, row_offsets, rows,
     mask_bits)`` receives each chip's device-packed rows and its processing masks as bit words
     [n_pix][words] (ccdgpu.abi.unpack_mask_bits; default sink: a SummarySink).  Returns the sink
-    and this process's statistics."""
+    and this process's statistics.  ``upload_depth``: batches each context keeps uploaded or
+    uploading ahead of the one it detects (1 .. ccdgpu.UPLOAD_SLOTS - 1)."""
     if context_factory is None:
         import ccdgpu
         context_factory = ccdgpu.Context
@@ -204,7 +209,8 @@ def detect_tile(xys, source, queue, device=0, contexts=2, batch_chips=16, params
     ctxs = [context_factory(device) for _ in range(max(1, int(contexts)))]
     t0 = time.perf_counter()
     try:
-        th = [threading.Thread(target=_worker, args=(c, queue, source, xys, batch_chips, params, width, sink, stats, errors))
+        th = [threading.Thread(target=_worker, args=(c, queue, source, xys, batch_chips, params, width, sink, stats, errors,
+                                                       max(1, int(upload_depth))))
               for c in ctxs]
         for t in th:
             t.start()
@@ -235,7 +241,7 @@ def gather(obj, dist=None):
 
 
 def changedetection(tile, source, device=None, contexts=2, batch_chips=16, number=None, params=None,
-                    sink=None, width=100, context_factory=None, ctx=None):
+                    sink=None, width=100, context_factory=None, ctx=None, upload_depth=2):
     """Change detection for a tile on every GPU of the job (reference core.changedetection,
     ccdc/core.py:78-123).
 
@@ -268,7 +274,8 @@ def changedetection(tile, source, device=None, contexts=2, batch_chips=16, numbe
         device = int(os.environ.get('LOCAL_RANK', '0'))
     log.info('change detection of %d chips, %d per launch, rank %d' % (len(xys), batch_chips, rank))
     sink, stats = detect_tile(xys, source, queue, device=device, contexts=contexts, batch_chips=batch_chips,
-                              params=params, width=width, sink=sink, context_factory=context_factory)
+                              params=params, width=width, sink=sink, context_factory=context_factory,
+                              upload_depth=upload_depth)
     stats['rank'] = rank
     chip_summaries = getattr(sink, 'chips', [])
     parts = gather((stats, chip_summaries), dist if dist_on else None)

@@ -14,6 +14,7 @@ import numpy as np
 from . import abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
+UPLOAD_SLOTS = 4  # CCDGPU_UPLOAD_SLOTS (include/ccdgpu.h): input slots per context
 LIB_PATH = os.environ.get('CCDGPU_LIBRARY') or os.path.join(os.path.dirname(_HERE), 'lib', 'libccdgpu.so')
 
 _lib = None
@@ -265,7 +266,7 @@ class Context(object):
         return batch
 
     def stage_slot_chips(self, slot, batch, params=None):
-        """Upload a ChipBatch into input slot 0/1 on the copy stream and return at once (the
+        """Upload a ChipBatch into input slot 0 .. UPLOAD_SLOTS-1 on the copy stream and return at once (the
         batch must stay alive and unchanged until run_slot(slot) returns; pinned=True batches
         upload asynchronously)."""
         p = params if isinstance(params, abi.Params) else abi.params_from_dict(params)
@@ -297,7 +298,7 @@ class Context(object):
             lib().ccdgpu_rows_free(ctypes.byref(r))
 
     def stage_slot(self, slot, dates, spectra, qa, params=None):
-        """Upload a batch into input slot 0/1 on the copy stream and return at once (the arrays
+        """Upload a batch into input slot 0 .. UPLOAD_SLOTS-1 on the copy stream and return at once (the arrays
         must stay alive and unchanged until run_slot(slot) returns; pinned arrays from
         ``pinned_empty`` make the upload overlap a running detection)."""
         dates, spectra, qa = _as_inputs(dates, spectra, qa)

@@ -77,6 +77,7 @@ struct __attribute__((aligned(16))) Lds {
     int y0[8];             // per-band value shift of the accumulated window
     union {                // Tmask (initialize) and the closest-DOY buckets (lookforward) never overlap
         uint32_t hist2[732];   // closest-DOY: fit-window counts per (4 t mod 1461) bin, 2 x u16 per word
+        uint16_t hist16[1464]; // the same bins read one u16 at a time (ds_read_u16: no shift / mask)
         struct {
             uint32_t tflag[MAXW];  // Tmask outlier flags of the current window
             double tchol[5][5];    // Tmask: Cholesky factor of the unweighted normal matrix
@@ -210,14 +211,26 @@ __device__ __forceinline__ unsigned long long ph_stamp() {
 #endif
 
 // ------------------------------------------------------------------ index guards
-// Every read of the compacted period goes through these: an out-of-range index is clamped (so a
-// logic error can never fault the GPU) and the offending source line is kept in a register
-// (P.bad); at the end of the pixel the wave publishes it to counters[4], which the host turns
-// into CCDGPU_EHIP naming the line.
+// Every read of the compacted period and of the slot scratch goes through these: an index past
+// the end is clamped into [0, lim) (one v_min_u32), so a logic error can never fault the GPU.
+// The checking build (-DCCD_GUARD_LINES, lib/libccdgpu_guard.so, run over the golden vectors by
+// tests/test_gpu_batches.py) also keeps the offending source line in a register (P.bad); at the
+// end of the pixel the wave publishes it to counters[4], which the host turns into CCDGPU_EHIP
+// naming the line.  (The line bookkeeping costs the product build ~2 %: a compare, two selects
+// and a live register per access.)
 __device__ __forceinline__ int gidx(const Px &P, int j, int lim, int line) {
+#if defined(CCD_NOGUARD)  // measurement build only: what the clamp costs
+    return j;
+#elif defined(CCD_GUARD_LINES)
     const bool ok = (unsigned)j < (unsigned)lim;
     P.bad = ok ? P.bad : line;
     return ok ? j : 0;
+#else
+    (void)P;
+    (void)line;
+    const unsigned u = (unsigned)j, c = (unsigned)(lim > 0 ? lim - 1 : 0);  // (lim: wave-uniform, SALU)
+    return (int)(u < c ? u : c);
+#endif
 }
 // physical row of logical row j (gap buffer)
 // (-DCCD_NO_GAP: no gap buffer -- a removal shifts the whole tail, rows never move otherwise)
@@ -633,6 +646,20 @@ __device__ __forceinline__ double gmax8(double v) {
     return vmax(v, dpp<0x141>(v));
 }
 
+// float max over a band's 8 lanes, one DPP-modified v_max_f32 per level (a 64-bit max needs two
+// lane moves and a max per level); s_nop 1: a DPP source read 2 wait states after its VALU write
+__device__ __forceinline__ float gmax8f(float v) {
+    float r;
+    asm("s_nop 1\n\t"
+        "v_max_f32_dpp %0, %1, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf"
+        : "=&v"(r) : "v"(v));
+    return r;
+}
+
 // One coordinate of the cyclic sweep (coordinate J of every band group).  Lane (b, k) holds
 // g_k = q_k - sum_m G_km w_m (the correlation X_k . R of sklearn's residual form); coordinate J's
 // update uses tmp = X_J . (R + w_J X_J) = g_J + G_JJ w_J, then every g_k absorbs the change.
@@ -679,6 +706,7 @@ __device__ __forceinline__ int cd_sweep(Lds *L, int pc_rt, double alpha, int max
     const double yy = b < NB ? L->YY[b] : 0.0;
     const double tol_s = tol * yy;
     const double tol_m = -0x1p-45 * tol;  // exact (a power of two)
+    const float tol_f = (float)tol;
     const bool can = act && gkk != 0.0;  // sklearn skips zero-norm columns
     double w = 0.0, g = q;
     bool done = b >= NB;
@@ -694,18 +722,38 @@ __device__ __forceinline__ int cd_sweep(Lds *L, int pc_rt, double alpha, int max
         if (pc > 4) cd_coord<4>(k, live, alpha, gkk, rgkk, gcol[4], g, w);
         if (pc > 5) cd_coord<5>(k, live, alpha, gkk, rgkk, gcol[5], g, w);
         if (pc > 6) cd_coord<6>(k, live, alpha, gkk, rgkk, gcol[6], g, w);
-        // every coordinate moves once per sweep: d_w_ii = |w_new - w_old| of the lane's own one
-        const double d_w_max = gmax8(fabs(w - w0));
-        const double w_max = gmax8(fabs(w));  // w stays 0 in lanes outside the model
-        // sklearn's d_w_max / w_max < tol (w_max = 0 is the check's own first clause).  The sign
-        // of the fused d_w_max - tol w_max (one rounding of the exact value) decides it outside a
-        // sliver of relative width 2^-45 around tol, where the quotient itself is taken:
-        // r >= 0 -> d/w >= tol -> fl(d/w) >= tol; r < -2^-45 tol w -> fl(d/w) < tol.
-        const double r = fma(-tol, w_max, d_w_max);
-        bool ratio_lt = r < tol_m * w_max;
-        const bool amb = !(r >= 0.0) && !ratio_lt;
-        if (bal(amb)) ratio_lt = amb ? d_w_max / w_max < tol : ratio_lt;
-        const bool check = !done && (w_max == 0.0 || ratio_lt || it == max_iter - 1);
+        // every coordinate moves once per sweep: d_w_ii = |w_new - w_old| of the lane's own one.
+        // sklearn's d_w_max / w_max < tol (w_max = 0 is the check's own first clause), decided
+        // first on the float32 roundings of the two maxima (max commutes with the monotone
+        // rounding, so they are fl32(d_w_max) and fl32(w_max), each within 2^-24 relative): with
+        // w_max in [2^-100, 2^100], D < fl(tol) W (1 - 2^-16) implies d/w < tol (1 - 2^-17), so
+        // fl64(d/w) < tol, and D > fl(tol) W (1 + 2^-16) implies fl64(d/w) >= tol.  Groups whose
+        // ratio falls in that band (or whose w_max is 0 or out of range) take the exact test.
+        bool ratio_lt, wzero = false;
+        {
+            const float D = gmax8f((float)fabs(w - w0));
+            const float Wf = gmax8f((float)fabs(w));  // w stays 0 in lanes outside the model
+            const float tw = tol_f * Wf;
+            const bool wok = Wf >= 0x1p-100f && Wf <= 0x1p100f;
+            const bool lt = wok && D < tw * (1.0f - 0x1p-16f);
+            const bool ge = wok && D > tw * (1.0f + 0x1p-16f);
+            ratio_lt = lt;
+            const bool amb32 = !done && !lt && !ge;
+            if (bal(amb32)) {
+                const double d_w_max = gmax8(fabs(w - w0));
+                const double w_max = gmax8(fabs(w));
+                // the sign of the fused d_w_max - tol w_max (one rounding of the exact value)
+                // decides it outside a sliver of relative width 2^-45 around tol, where the
+                // quotient itself is taken: r >= 0 -> fl(d/w) >= tol; r < -2^-45 tol w -> fl(d/w) < tol.
+                const double r = fma(-tol, w_max, d_w_max);
+                bool ex = r < tol_m * w_max;
+                const bool amb = !(r >= 0.0) && !ex;
+                if (bal(amb)) ex = amb ? d_w_max / w_max < tol : ex;
+                ratio_lt = amb32 ? ex : ratio_lt;
+                wzero = amb32 && w_max == 0.0;
+            }
+        }
+        const bool check = !done && (wzero || ratio_lt || it == max_iter - 1);
         if (bal(check)) {
             const double xta = act ? g : 0.0;  // X^T R
             const double dual = gmax8(fabs(xta));
@@ -1816,7 +1864,7 @@ __device__ __forceinline__ unsigned det_mask() { return ARGS().p.detection_bands
 __device__ __forceinline__ int fs_width(unsigned dm) { return __builtin_popcount(dm) <= 5 ? 5 : 7; }
 // L->hist2 holds two u16 per word: plain counts (closest_doy_scan) or, after build_closest, the
 // end position of each bin in the bucket list.
-__device__ __forceinline__ int h16(const Lds *L, int u) { return (int)((L->hist2[u >> 1] >> ((u & 1) * 16)) & 0xFFFFu); }
+__device__ __forceinline__ int h16(const Lds *L, int u) { return (int)L->hist16[u]; }  // = hist2[u/2] half u%2
 __device__ __forceinline__ int bend(const Lds *L, int u) { return h16(L, u); }
 __device__ __forceinline__ int bstart(const Lds *L, int u) { return u == 0 ? 0 : h16(L, u - 1); }
 __device__ __forceinline__ int bcount(const Lds *L, int u) { return bend(L, u) - bstart(L, u); }
@@ -2053,6 +2101,38 @@ __device__ __forceinline__ int cnt_within(const Lds *L, int nf, int u, int d) {
     return d >= 730 ? nf : c;
 }
 
+// cs[bd] += p[s * FW + bd] for s = 0 .. cnt - 1, in order (cnt per lane).
+#ifndef CCD_RS
+#define CCD_RS 4
+#endif
+template <int FW>
+__device__ __forceinline__ void run_add(const GLOBAL_AS double *p, int cnt, double (&cs)[NB]) {
+    constexpr int RS = CCD_RS;
+    int s = 0;
+    for (; s + RS <= cnt; s += RS) {
+        double f[RS][FW];
+#pragma unroll
+        for (int u = 0; u < RS; ++u) {
+#pragma unroll
+            for (int bd = 0; bd < FW; ++bd) f[u][bd] = p[u * FW + bd];
+        }
+#pragma unroll
+        for (int u = 0; u < RS; ++u) {
+#pragma unroll
+            for (int bd = 0; bd < FW; ++bd) cs[bd] += f[u][bd];
+        }
+        p += RS * FW;
+    }
+    for (; s < cnt; ++s) {
+        double f[FW];
+#pragma unroll
+        for (int bd = 0; bd < FW; ++bd) f[bd] = p[bd];
+#pragma unroll
+        for (int bd = 0; bd < FW; ++bd) cs[bd] += f[bd];
+        p += FW;
+    }
+}
+
 // Per-lane find_closest_doy(period, ref, fit_window, 24) comparison rmse (change.lookforward):
 // the 24 fit-window observations closest in day of year to date dref, sqrt(sum r^2) / 4 per band,
 // from the bucket list and bucket-ordered squared residuals build_closest left (nf > 24).
@@ -2080,33 +2160,15 @@ __device__ __forceinline__ void comp_lane(Px &P, int nf, int dref, double (&cs)[
     const int s0 = K > 0 ? bstart(L, (u - K + 1 + 1461) % 1461) : 0;
     PH_END(P, c1, 21)
     PH_BEGIN(c2)
-    // Rounds of RS rows: every row's loads are issued before the first add (the rows of a round
-    // beyond `less` re-read row 0 and are added with weight 0: fma(f, 1, c) is the plain add, so
-    // the sum stays exactly the bucket-order sum).
-#ifndef CCD_RS
-#define CCD_RS 4
-#endif
-    constexpr int RS = CCD_RS;
-    const int s0w = s0 >= nf ? s0 - nf : s0;  // bucket position of row 0 (s0 may equal nf)
-    for (int s = 0; s < less; s += RS) {
-        double f[RS][FW];
-        double wt[RS];
-#pragma unroll
-        for (int u = 0; u < RS; ++u) {
-            int pos = s0 + s + u;
-            pos = pos >= nf ? pos - nf : pos;
-            const bool ok = s + u < less;
-            wt[u] = ok ? 1.0 : 0.0;
-            const GLOBAL_AS double *fp = P.fs + (size_t)gidx(P, ok ? pos : s0w, nf, __LINE__) * FW;
-#pragma unroll
-            for (int bd = 0; bd < FW; ++bd) f[u][bd] = fp[bd];
-        }
-#pragma unroll
-        for (int u = 0; u < RS; ++u) {
-#pragma unroll
-            for (int bd = 0; bd < FW; ++bd) cs[bd] = fma(f[u][bd], wt[u], cs[bd]);
-        }
-    }
+    // The run is at most two contiguous stretches of bucket positions (it wraps at nf at most
+    // once): [s0w, s0w + n1) and [0, less - n1), summed in that order (= bucket order).  A stretch
+    // is read in rounds of RS rows from one running address, every row's loads at an immediate
+    // offset and issued before the first add; no per-row index arithmetic.
+    const int s0w = gidx(P, s0 >= nf ? s0 - nf : s0, nf, __LINE__);  // bucket position of row 0
+    const int lr = less < nf ? less : nf;
+    const int n1 = lr < nf - s0w ? lr : nf - s0w;
+    run_add<FW>(P.fs + (size_t)s0w * FW, n1, cs);
+    run_add<FW>(P.fs, lr - n1, cs);
     PH_END(P, c2, 22)
     PH_BEGIN(c3)
     const int b1 = (u - K + 1461) % 1461, b2 = (u + K) % 1461;

@@ -140,7 +140,7 @@ struct ccdgpu_ctx {
     int arg_slot = -1;  // this context's launch-argument slot in constant memory
     hipStream_t stream = nullptr;
     hipStream_t copy_stream = nullptr;  // uploads of ccdgpu_stage_slot (overlap a running detection)
-    hipEvent_t uploaded[2] = {nullptr, nullptr};
+    hipEvent_t uploaded[CCDGPU_UPLOAD_SLOTS] = {};
     // inputs the next detection reads: the single staged batch, or one of the two upload slots
     const int64_t *in_dates = nullptr;
     const int16_t *in_spectra = nullptr;
@@ -169,12 +169,12 @@ struct ccdgpu_ctx {
     DevBuf<int64_t> row_off, seg_off1;
     DevBuf<int32_t> row_xy;     // per-chip (cx, cy) of a batch row fetch
     DevBuf<int8_t> mask8;
-    DevBuf<int64_t> slot_dates[2];   // double-buffered inputs (ccdgpu_stage_slot / ccdgpu_run_slot)
-    DevBuf<int16_t> slot_spectra[2];
-    DevBuf<uint16_t> slot_qa[2];
-    Shape slot_shape[2];
-    ccdgpu_params slot_params[2];
-    bool slot_ready[2] = {false, false};
+    DevBuf<int64_t> slot_dates[CCDGPU_UPLOAD_SLOTS];   // upload slots (ccdgpu_stage_slot / ccdgpu_run_slot)
+    DevBuf<int16_t> slot_spectra[CCDGPU_UPLOAD_SLOTS];
+    DevBuf<uint16_t> slot_qa[CCDGPU_UPLOAD_SLOTS];
+    Shape slot_shape[CCDGPU_UPLOAD_SLOTS];
+    ccdgpu_params slot_params[CCDGPU_UPLOAD_SLOTS];
+    bool slot_ready[CCDGPU_UPLOAD_SLOTS] = {};
     DevBuf<unsigned char> b64;  // chipmunk payload text of the last ccdgpu_stage_chipmunk
     DevBuf<int64_t> b64_off;
     std::vector<int64_t> h_offsets;
@@ -196,7 +196,7 @@ struct ccdgpu_ctx {
         csr.release();
         cub_tmp.release();
         b64.release();
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < CCDGPU_UPLOAD_SLOTS; ++i) {
             slot_dates[i].release();
             slot_spectra[i].release();
             slot_qa[i].release();
@@ -500,7 +500,8 @@ int ccdgpu_stage_slot_chips(ccdgpu_ctx *c, int32_t slot, const ccdgpu_params *pa
                             const int32_t *n_pix, const int32_t *n_obs, const int64_t *dates, const int16_t *spectra,
                             const uint16_t *qa) {
     if (!c) return fail(CCDGPU_EINVAL, "NULL ctx");
-    if (slot < 0 || slot > 1) return fail(CCDGPU_EINVAL, "slot must be 0 or 1");
+    if (slot < 0 || slot >= CCDGPU_UPLOAD_SLOTS)
+        return fail(CCDGPU_EINVAL, "slot must be in 0 .. " + std::to_string(CCDGPU_UPLOAD_SLOTS - 1));
     if (!dates || !spectra || !qa) return fail(CCDGPU_EINVAL, "NULL input buffer");
     Shape sh;
     int rc = make_shape(n_chips, n_pix, n_obs, sh);
@@ -531,7 +532,7 @@ int ccdgpu_stage_slot(ccdgpu_ctx *c, int32_t slot, const ccdgpu_params *params, 
 
 int ccdgpu_run_slot(ccdgpu_ctx *c, int32_t slot, double *kernel_seconds) {
     if (!c) return fail(CCDGPU_EINVAL, "NULL ctx");
-    if (slot < 0 || slot > 1 || !c->slot_ready[slot]) return fail(CCDGPU_EINVAL, "slot has no staged batch");
+    if (slot < 0 || slot >= CCDGPU_UPLOAD_SLOTS || !c->slot_ready[slot]) return fail(CCDGPU_EINVAL, "slot has no staged batch");
     int rc = stage_alloc(c, &c->slot_params[slot], c->slot_shape[slot], nullptr, false);
     if (rc) return rc;
     HIPCHK(hipStreamWaitEvent(c->stream, c->uploaded[slot], 0));

@@ -56,3 +56,8 @@ def test_init_without_gpu_fails_loudly():
         pytest.skip('a GPU is visible')
     with pytest.raises(ccdgpu.CcdGpuError):
         ccdgpu.Context(0)
+
+
+def test_header_constants_match_the_binding():
+    txt = open(os.path.join(ROOT, 'include', 'ccdgpu.h')).read()
+    assert int(re.search(r'#define CCDGPU_UPLOAD_SLOTS (\d+)', txt).group(1)) == ccdgpu.UPLOAD_SLOTS

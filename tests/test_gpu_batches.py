@@ -239,3 +239,47 @@ def test_kernel_variants_and_poisoned_scratch_are_identical():
     for (d, s, q), params, ref in cases:
         assert_parity(c.detect_batch(d, s, q, params=params), ref)
     c.close()
+
+
+_GUARD_SCRIPT = r'''
+import hashlib, os, sys
+sys.path[:0] = sys.argv[1:]
+import ccdgpu, golden_util
+from ccdgpu import synth
+c = ccdgpu.Context(0)
+h = hashlib.sha256()
+for name in golden_util.names():
+    (d, s, q), params, _ = golden_util.load(name)
+    u = c.detect_batch(d, s, q, params=params)
+    for a in (u.seg_offsets, u.segments, u.mask, u.procedure):
+        h.update(a.tobytes())
+for which, chip, n_pix in ((5, 3, 1500), (3, 4, 1500), (4, 11, 1500)):
+    d, s, q = synth.chip(synth.config(which), chip, 0, n_pix)
+    u = c.detect_batch(d, s, q)
+    for a in (u.seg_offsets, u.segments, u.mask, u.procedure):
+        h.update(a.tobytes())
+c.close()
+print(h.hexdigest())
+'''
+
+
+def test_guard_lines_build_trips_no_guard_and_matches_product():
+    """The product kernel clamps out-of-range period / scratch indices without recording them;
+    the checking build (lib/libccdgpu_guard.so, -DCCD_GUARD_LINES) raises CCDGPU_EHIP naming the
+    source line of any tripped guard.  Run in a child process (the library is chosen at load),
+    it must trip none on the golden vectors and three synthetic chips (C3 sidelap, C4 high-cloud,
+    C5 change-dense), and give byte-identical results to the product build."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    guard = os.path.join(root, 'lcmap-firebird_amd', 'lib', 'libccdgpu_guard.so')
+    assert os.path.exists(guard), 'build lib/libccdgpu_guard.so (make -C lcmap-firebird_amd)'
+    paths = [os.path.join(root, 'lcmap-firebird_amd'), os.path.join(root, 'tests')]
+    outs = []
+    for lib in (guard, ccdgpu.LIB_PATH):
+        env = dict(os.environ, CCDGPU_LIBRARY=lib)
+        r = subprocess.run([sys.executable, '-c', _GUARD_SCRIPT] + paths, env=env, capture_output=True,
+                           text=True, timeout=300)
+        assert r.returncode == 0, (lib, r.stderr[-2000:])
+        outs.append(r.stdout.strip().splitlines()[-1])
+    assert outs[0] == outs[1]
