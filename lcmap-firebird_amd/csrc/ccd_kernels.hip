@@ -661,29 +661,38 @@ __device__ __forceinline__ float gmax8f(float v) {
 }
 
 // One coordinate of the cyclic sweep (coordinate J of every band group).  Lane (b, k) holds
-// g_k = q_k - sum_m G_km w_m (the correlation X_k . R of sklearn's residual form); coordinate J's
-// update uses tmp = X_J . (R + w_J X_J) = g_J + G_JJ w_J, then every g_k absorbs the change.
+// h_k = g_k + G_kk w_k, where g_k = q_k - sum_m G_km w_m is the correlation X_k . R of sklearn's
+// residual form: h_J is sklearn's tmp = X_J . (R + w_J X_J) for coordinate J as it stands, so the
+// update reads it directly.  A change d of w_J moves h_k by -G_kJ d for k != J and leaves h_J as
+// it is (the G_JJ terms cancel), so the broadcast column carries a zero on its diagonal.
+// Per coordinate: soft threshold (3 VALU), d (1 fused), lane J's w (1, exec-masked), 2 DPP FMAs.
 template <int J>
-__device__ __forceinline__ void cd_coord(int k, bool live, double alpha, double gkk, double rgkk,
-                                         double ngcolJ, double &g, double &w) {
-#pragma clang fp contract(off)  // d = wn - w rounded as w's own update (no fma with the product)
-    const double tmp = fma(gkk, w, g);
+__device__ __forceinline__ void cd_coord(unsigned long long mJ /* live lanes of coordinate J */,
+                                         double alpha, double rgkk, double ngcolJ, double &h, double &w) {
     // sklearn: fsign(tmp) * fmax(|tmp| - alpha, 0) / norm (a signed zero below alpha, as there)
-    const double wn = copysign(fmax(fabs(tmp) - alpha, 0.0), tmp) * rgkk;
-    // d is read from lane J only; a finished group's gcol is zero, so d needs no gating and the
-    // select of w stays off the chain into the FMAs
-    const double d = wn - w;
-    w = (live && k == J) ? wn : w;
-    // g += (-G_kJ) * d_J: two 64-bit DPP FMAs, row_newbcast (lane J of the 16-lane row to the
+    const double s = copysign(fmax(fabs(h) - alpha, 0.0), h);
+    // d = w_new - w_old in one rounding (read from lane J only; a finished group's column is
+    // zero, so d needs no gating)
+    const double d = fma(s, rgkk, -w);
+    // w_J = S(tmp) / G_JJ as a multiply, in the live lanes of coordinate J only: one VALU under
+    // an exec mask instead of a 64-bit select (two v_cndmask).  s_and_saveexec keeps any lane the
+    // caller had disabled disabled.
+    unsigned long long sv;
+    asm volatile("s_and_saveexec_b64 %[sv], %[m]\n\t"
+                 "v_mul_f64 %[w], %[s], %[r]\n\t"
+                 "s_mov_b64 exec, %[sv]"
+                 : [w] "+v"(w), [sv] "=&s"(sv)
+                 : [m] "s"(mJ), [s] "v"(s), [r] "v"(rgkk));
+    // h += (-G_kJ) * d_J: two 64-bit DPP FMAs, row_newbcast (lane J of the 16-lane row to the
     // row) with the bank mask of the band group that owns that lane -- lanes 0-7 of each row take
     // lane J, lanes 8-15 lane 8 + J.  s_nop 1 before each: a DPP FMA reads its operands (the
     // accumulator included) 2 wait states behind a VALU write of them -- back to back, the second
     // FMA loses the first one's result (tools/probe/dpp64.hip, measured on gfx950).
-    asm("s_nop 1\n\t"
-        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0x3\n\t"
-        "s_nop 1\n\t"
-        "v_fmac_f64_dpp %0, %1, %2 row_newbcast:%4 row_mask:0xf bank_mask:0xc"
-        : "+v"(g) : "v"(d), "v"(ngcolJ), "i"(J), "i"(J + 8));
+    asm volatile("s_nop 1\n\t"
+                 "v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0x3\n\t"
+                 "s_nop 1\n\t"
+                 "v_fmac_f64_dpp %0, %1, %2 row_newbcast:%4 row_mask:0xf bank_mask:0xc"
+                 : "+v"(h) : "v"(d), "v"(ngcolJ), "i"(J), "i"(J + 8));
 }
 
 // sklearn 0.18 enet_coordinate_descent (beta = 0, cyclic, duality-gap stop) in gradient form,
@@ -698,8 +707,9 @@ __device__ __forceinline__ int cd_sweep(Lds *L, int pc_rt, double alpha, int max
     const int b = l >> 3, k = l & 7;
     const bool act = b < NB && k < pc;
     double gcol[7];
+    // negated (h += gcol * d), zero on the diagonal (a coordinate's own h does not move)
 #pragma unroll
-    for (int j = 0; j < 7; ++j) gcol[j] = (act && j < pc) ? -L->G[j][k] : 0.0;  // negated: g += gcol * d
+    for (int j = 0; j < 7; ++j) gcol[j] = (act && j < pc && j != k) ? -L->G[j][k] : 0.0;
     const double gkk = act ? L->G[k][k] : 0.0;
     const double rgkk = gkk != 0.0 ? 1.0 / gkk : 0.0;  // w_k = S(tmp, alpha) / G_kk as a multiply
     const double q = act ? L->Q[k][b] : 0.0;
@@ -708,20 +718,25 @@ __device__ __forceinline__ int cd_sweep(Lds *L, int pc_rt, double alpha, int max
     const double tol_m = -0x1p-45 * tol;  // exact (a power of two)
     const float tol_f = (float)tol;
     const bool can = act && gkk != 0.0;  // sklearn skips zero-norm columns
-    double w = 0.0, g = q;
-    bool done = b >= NB;
+    // coordinate J's lanes (b, J), b < 7: one bit per band group
+    constexpr unsigned long long COL = 0x0001010101010101ull;
+    double w = 0.0, h = q;  // h = g + G_kk w = q at w = 0
+    // loop control in wave-uniform lane masks (SALU): finished groups (all 8 lanes of a band
+    // whose duality gap met tol, and lanes 56-63), and the lanes sklearn updates at all
+    unsigned long long dmask = bal(b >= NB);
+    const unsigned long long cmask = bal(can);
     int sweeps = max_iter;
     for (int it = 0; it < max_iter; ++it) {
-        if (bal(!done) == 0ull) break;
-        const bool live = can && !done;
+        if (dmask == ~0ull) break;
+        const unsigned long long lm = cmask & ~dmask;  // live lanes (all coordinates)
         const double w0 = w;
-        cd_coord<0>(k, live, alpha, gkk, rgkk, gcol[0], g, w);
-        if (pc > 1) cd_coord<1>(k, live, alpha, gkk, rgkk, gcol[1], g, w);
-        if (pc > 2) cd_coord<2>(k, live, alpha, gkk, rgkk, gcol[2], g, w);
-        if (pc > 3) cd_coord<3>(k, live, alpha, gkk, rgkk, gcol[3], g, w);
-        if (pc > 4) cd_coord<4>(k, live, alpha, gkk, rgkk, gcol[4], g, w);
-        if (pc > 5) cd_coord<5>(k, live, alpha, gkk, rgkk, gcol[5], g, w);
-        if (pc > 6) cd_coord<6>(k, live, alpha, gkk, rgkk, gcol[6], g, w);
+        cd_coord<0>(lm & COL, alpha, rgkk, gcol[0], h, w);
+        if (pc > 1) cd_coord<1>(lm & (COL << 1), alpha, rgkk, gcol[1], h, w);
+        if (pc > 2) cd_coord<2>(lm & (COL << 2), alpha, rgkk, gcol[2], h, w);
+        if (pc > 3) cd_coord<3>(lm & (COL << 3), alpha, rgkk, gcol[3], h, w);
+        if (pc > 4) cd_coord<4>(lm & (COL << 4), alpha, rgkk, gcol[4], h, w);
+        if (pc > 5) cd_coord<5>(lm & (COL << 5), alpha, rgkk, gcol[5], h, w);
+        if (pc > 6) cd_coord<6>(lm & (COL << 6), alpha, rgkk, gcol[6], h, w);
         // every coordinate moves once per sweep: d_w_ii = |w_new - w_old| of the lane's own one.
         // sklearn's d_w_max / w_max < tol (w_max = 0 is the check's own first clause), decided
         // first on the float32 roundings of the two maxima (max commutes with the monotone
@@ -729,17 +744,18 @@ __device__ __forceinline__ int cd_sweep(Lds *L, int pc_rt, double alpha, int max
         // w_max in [2^-100, 2^100], D < fl(tol) W (1 - 2^-16) implies d/w < tol (1 - 2^-17), so
         // fl64(d/w) < tol, and D > fl(tol) W (1 + 2^-16) implies fl64(d/w) >= tol.  Groups whose
         // ratio falls in that band (or whose w_max is 0 or out of range) take the exact test.
-        bool ratio_lt, wzero = false;
+        unsigned long long rl, wz = 0ull;  // groups with d_w_max / w_max < tol, with w_max = 0
         {
             const float D = gmax8f((float)fabs(w - w0));
             const float Wf = gmax8f((float)fabs(w));  // w stays 0 in lanes outside the model
             const float tw = tol_f * Wf;
-            const bool wok = Wf >= 0x1p-100f && Wf <= 0x1p100f;
-            const bool lt = wok && D < tw * (1.0f - 0x1p-16f);
-            const bool ge = wok && D > tw * (1.0f + 0x1p-16f);
-            ratio_lt = lt;
-            const bool amb32 = !done && !lt && !ge;
-            if (bal(amb32)) {
+            // (one ballot per comparison: each v_cmp writes its lane mask straight to SGPRs)
+            const unsigned long long wokm = bal(Wf >= 0x1p-100f) & bal(Wf <= 0x1p100f);
+            const unsigned long long ltm = wokm & bal(D < tw * (1.0f - 0x1p-16f));
+            const unsigned long long gem = wokm & bal(D > tw * (1.0f + 0x1p-16f));
+            rl = ltm;
+            const unsigned long long ambm = ~dmask & ~ltm & ~gem;
+            if (ambm) {
                 const double d_w_max = gmax8(fabs(w - w0));
                 const double w_max = gmax8(fabs(w));
                 // the sign of the fused d_w_max - tol w_max (one rounding of the exact value)
@@ -749,13 +765,13 @@ __device__ __forceinline__ int cd_sweep(Lds *L, int pc_rt, double alpha, int max
                 bool ex = r < tol_m * w_max;
                 const bool amb = !(r >= 0.0) && !ex;
                 if (bal(amb)) ex = amb ? d_w_max / w_max < tol : ex;
-                ratio_lt = amb32 ? ex : ratio_lt;
-                wzero = amb32 && w_max == 0.0;
+                rl = (rl & ~ambm) | (bal(ex) & ambm);
+                wz = bal(w_max == 0.0) & ambm;
             }
         }
-        const bool check = !done && (wzero || ratio_lt || it == max_iter - 1);
-        if (bal(check)) {
-            const double xta = act ? g : 0.0;  // X^T R
+        const unsigned long long chk = ~dmask & (wz | rl | (it == max_iter - 1 ? ~0ull : 0ull));
+        if (chk) {
+            const double xta = act ? fma(-gkk, w, h) : 0.0;  // X^T R = g = h - G_kk w
             const double dual = gmax8(fabs(xta));
             const double wq = gsum8(w * q);
             const double wxta = gsum8(w * xta);
@@ -771,11 +787,13 @@ __device__ __forceinline__ int cd_sweep(Lds *L, int pc_rt, double alpha, int max
                 gap = rr;
             }
             gap += alpha * l1 - cst * ry;
-            if (check && gap < tol_s) {
-                done = true;
-                sweeps = it + 1;
+            const unsigned long long fin = chk & bal(gap < tol_s);
+            if (fin) {
+                const bool f = (fin >> l) & 1ull;
+                sweeps = f ? it + 1 : sweeps;
 #pragma unroll
-                for (int j = 0; j < 7; ++j) gcol[j] = 0.0;  // g and w of the group stay as they are
+                for (int j = 0; j < 7; ++j) gcol[j] = f ? 0.0 : gcol[j];  // h and w of the group stay as they are
+                dmask |= fin;
             }
         }
     }
@@ -2329,7 +2347,9 @@ __device__ __forceinline__ void spec_fits(Px &P, int a, int nw0, int V, SpecFit 
     const double alpha = p.lasso_alpha * (double)nv;
     const double tol = p.lasso_tol, tol_s = tol * yy;
     const int max_iter = p.lasso_max_iter;
-    double rg[SPEC_PC], w[SPEC_PC], g[SPEC_PC];
+    // h_i = g_i + G_ii w_i (sklearn's tmp for coordinate i), as in cd_coord: a change of w_i moves
+    // every other h_m by -G_mi d and leaves h_i as it is
+    double rg[SPEC_PC], w[SPEC_PC], h[SPEC_PC];
     bool can[SPEC_PC];
 #pragma unroll
     for (int i = 0; i < SPEC_PC; ++i) {
@@ -2337,7 +2357,7 @@ __device__ __forceinline__ void spec_fits(Px &P, int a, int nw0, int V, SpecFit 
         rg[i] = gd != 0.0 ? 1.0 / gd : 0.0;
         can[i] = act && i < pc && gd != 0.0;  // sklearn skips zero-norm columns
         w[i] = 0.0;
-        g[i] = q[i];
+        h[i] = q[i];
     }
     const bool any5 = bal(act && pc > 3) != 0ull;
     bool done = !act;
@@ -2348,15 +2368,15 @@ __device__ __forceinline__ void spec_fits(Px &P, int a, int nw0, int V, SpecFit 
 #pragma unroll
         for (int i = 0; i < SPEC_PC; ++i) {
             if (i >= 3 && !any5) break;
-            const double tmp = g[i] + G[ut(i, i)] * w[i];
-            const double wn = copysign(fmax(fabs(tmp) - alpha, 0.0), tmp) * rg[i];
+            const double wn = copysign(fmax(fabs(h[i]) - alpha, 0.0), h[i]) * rg[i];
             const bool upd = !done && can[i];
             const double wnew = upd ? wn : w[i];
             const double d = wnew - w[i];
             w[i] = wnew;
             dmax = fmax(dmax, fabs(d));
 #pragma unroll
-            for (int m = 0; m < SPEC_PC; ++m) g[m] -= G[m < i ? ut(m, i) : ut(i, m)] * d;
+            for (int m = 0; m < SPEC_PC; ++m)
+                if (m != i) h[m] -= G[m < i ? ut(m, i) : ut(i, m)] * d;
         }
         double wmax = 0.0;
 #pragma unroll
@@ -2367,9 +2387,10 @@ __device__ __forceinline__ void spec_fits(Px &P, int a, int nw0, int V, SpecFit 
             double dual = 0.0, wq = 0.0, wxta = 0.0, l1 = 0.0;
 #pragma unroll
             for (int i = 0; i < SPEC_PC; ++i) {
-                if (i < pc) dual = fmax(dual, fabs(g[i]));
+                const double g = h[i] - G[ut(i, i)] * w[i];  // X_i . R
+                if (i < pc) dual = fmax(dual, fabs(g));
                 wq += w[i] * q[i];
-                wxta += w[i] * g[i];
+                wxta += w[i] * g;
                 l1 += fabs(w[i]);
             }
             const double ry = yy - wq, rr = ry - wxta;

@@ -13,7 +13,7 @@ run_smoke() { timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(
 run_bench() { timeout -k 10 600 python bench.py > "$OUT/${TAG}_bench.json" 2> "$OUT/${TAG}_bench.err"; }
 run_prof() {
   ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
-      -d "$OUT/${TAG}_prof" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-stream --no-packer --contexts 1 \
+      -d "$OUT/${TAG}_prof" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-stream --no-packer --no-tile --contexts 1 \
       > "$OUT/${TAG}_prof.log" 2>&1 )
 }
 case "$STEPS" in
