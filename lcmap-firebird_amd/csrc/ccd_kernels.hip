@@ -2455,6 +2455,37 @@ __device__ __forceinline__ void spec_install(Px &P, const SpecFit &F, int s, int
     wsync();
 }
 
+// change_magnitude of the batched steps' peek observations (lane = step, ring PRES): allc =
+// every peek observation's magnitude exceeds the change threshold, outj = the first one's exceeds
+// the outlier threshold.  ND = number of detection bands read (5 for the default bands: the rows
+// past them would add 0).  One peek observation per round: its ND ring reads go out together.
+// The lane's ring address is re-derived every round (lane() is opaque), so no per-lane address
+// stays live across the loop for the allocator to spill -- a spilled one cost a scratch reload
+// and a full wait before every read.
+template <int ND>
+__device__ __forceinline__ void peek_mags(const int (&bs)[NB], const double (&irm)[NB], int k, bool &allc,
+                                          bool &outj) {
+    Lds *L = &LDS();
+    allc = true;
+    for (int j = 0; j < k; ++j) {
+        const double *Rj = PRES(L) + lane() + j;
+        double rv[ND];
+#pragma unroll
+        for (int t = 0; t < ND; ++t) rv[t] = Rj[bs[t] * PSTR];
+        double mg = 0.0;
+#pragma unroll
+        for (int t = 0; t < ND; ++t) {
+            const double v = rv[t] * irm[t];
+            mg += v * v;
+        }
+        allc = allc && mg > L->chg;
+        if (j == 0) outj = mg > ARGS().p.outlier_threshold;
+        // the remaining peek observations decide nothing once no lane can still detect a change
+        // (outj is fixed at j = 0; the ring keeps every residual for the medians)
+        if (bal(allc) == 0ull) break;
+    }
+}
+
 __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
     const ccdgpu_params &p = ARGS().p;
     Lds *L = &LDS();
@@ -2656,26 +2687,8 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
                 const double rm = (vr != vr || cr != cr) ? __builtin_nan("") : (vr > cr ? vr : cr);
                 irm[t] = t < nd ? 1.0 / rm : 0.0;
             }
-            allc = true;
-            // One peek observation per round: its 7 ring reads go out together (a band past the
-            // detection bands reads band 0's row and adds 0: irm is 0 there, ring rows are
-            // finite).  The lane's ring address is re-derived every round (lane() is opaque), so
-            // no per-lane address stays live across the loop for the allocator to spill -- a
-            // spilled one cost a scratch reload and a full wait before every read.
-            for (int j = 0; j < k; ++j) {
-                const double *Rj = PRES(L) + lane() + j;
-                double rv[NB];
-#pragma unroll
-                for (int t = 0; t < NB; ++t) rv[t] = Rj[bs[t] * PSTR];
-                double mg = 0.0;
-#pragma unroll
-                for (int t = 0; t < NB; ++t) {
-                    const double v = rv[t] * irm[t];
-                    mg += v * v;
-                }
-                allc = allc && mg > L->chg;
-                if (j == 0) outj = mg > p.outlier_threshold;
-            }
+            if (nd <= 5) peek_mags<5>(bs, irm, k, allc, outj);
+            else peek_mags<NB>(bs, irm, k, allc, outj);
             PH_END(P, mg, 15)
         }
         const unsigned long long O = bal(valid && outj);
