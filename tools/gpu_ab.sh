@@ -1,12 +1,16 @@
 #!/bin/bash
-# A/B of detection-library builds on the GPU box (developer tool): GPU parity tests of the default
-# build, then golden parity + a short C3 bench of each library named in LIBS (lib/<name>.so).
-set -o pipefail
-R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; OUT="$R/gpurun_out"; mkdir -p "$OUT"; TAG=${1:-ab}
-timeout -k 10 600 python -u -m pytest tests/test_gpu.py -x -v --timeout 120 --timeout-method thread -k "golden or chip_vs_oracle or param_variants" > "$OUT/${TAG}_pytest.log" 2>&1 || { echo "rc=$? tests" > "$OUT/${TAG}_rc.txt"; exit 1; }
-for name in ${LIBS:-libccdgpu}; do
-  export CCDGPU_LIBRARY="$R/lcmap-firebird_amd/lib/$name.so"
-  timeout -k 10 300 python -u -m pytest tests/test_gpu.py -x -q --timeout 120 --timeout-method thread -k "golden" > "$OUT/${TAG}_${name}_golden.log" 2>&1 || { echo "rc=$? golden $name" > "$OUT/${TAG}_rc.txt"; exit 1; }
-  timeout -k 10 300 python bench.py --steps 3 --no-cpu-baseline --no-stream --no-packer ${BENCH_ARGS} > "$OUT/${TAG}_${name}.json" 2> "$OUT/${TAG}_${name}.err" || { echo "rc=$? bench $name" > "$OUT/${TAG}_rc.txt"; exit 1; }
+# Developer tool: GPU suite at the working tree, then resident A/B of the kernel libraries in LIBS
+# (lib/<name>.so) on the C3 tile mix and, with C5=1, on the change-dense C5 chips.  Each GPU step
+# has its own time limit; the first failure ends the session.
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
+mkdir -p gpurun_out
+T=${TAG:-ab}
+[ -n "$SKIP_TESTS" ] || timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${T}_pytest.log 2>&1 || { echo "pytest rc=$?"; tail -30 gpurun_out/${T}_pytest.log; exit 1; }
+tail -2 gpurun_out/${T}_pytest.log
+Q="--steps ${STEPS:-4} --no-cpu-baseline --no-tile --no-stream --no-packer"
+for cfg in 3 ${C5:+5}; do
+  for n in ${LIBS:-libccdgpu}; do
+    CCDGPU_LIBRARY=$PWD/lcmap-firebird_amd/lib/$n.so timeout -k 10 300 python -u bench.py $Q --config $cfg > gpurun_out/${T}_c${cfg}_$n.json 2> gpurun_out/${T}_c${cfg}_$n.err || { echo "bench rc=$? $n"; tail -20 gpurun_out/${T}_c${cfg}_$n.err; exit 1; }
+    python -c "import json; b=json.load(open('gpurun_out/${T}_c${cfg}_$n.json')); print('C$cfg', '$n', round(b['value']), round(b['roofline']['frac'],4), round(b['roofline']['kernel_ms_per_launch'],1))"
+  done
 done
-echo rc=0 > "$OUT/${TAG}_rc.txt"
