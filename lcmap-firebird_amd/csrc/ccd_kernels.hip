@@ -2196,39 +2196,55 @@ __device__ __forceinline__ void comp_lane(Px &P, int nf, int dref, double (&cs)[
     // every entry at distance K is taken when there are no more of them than needed (no ranks)
     const bool all_k = T <= need;
     constexpr int TU = 8;
+    // Tb: the wave's largest T among the lanes on this path (uniform), so the entry loops below
+    // stop where every lane's entries end (T is 1 or 2 nearly always)
+    int Tb = 0;
+#pragma unroll
+    for (int e = 0; e < TU; ++e)
+        if (bal(T > e && T <= TU)) Tb = e + 1;
     if (T <= TU) {
         // up to 8 entries: their fit indices loaded at once and ranked in registers, then their
-        // squared residuals added in entry order (weight 0 for the entries not taken)
+        // squared residuals added in entry order (weight 0 for the entries not taken); ranks are
+        // needed only where more entries sit at distance K than are taken
         int iv[TU], pe[TU];
 #pragma unroll
         for (int e = 0; e < TU; ++e) {
             pe[e] = e < T ? (e < c1 ? st1 + e : st2 + (e - c1)) : 0;
             pe[e] = gidx(P, pe[e], nf, __LINE__);
         }
+        const bool rk = bal(!all_k) != 0ull;
 #pragma unroll
-        for (int e = 0; e < TU; ++e) iv[e] = (!all_k && e < T) ? (int)P.bk[pe[e]] : 0x7FFFFFFF;
+        for (int e = 0; e < TU; ++e) {
+            iv[e] = 0x7FFFFFFF;
+            if (rk && e < Tb) iv[e] = (!all_k && e < T) ? (int)P.bk[pe[e]] : 0x7FFFFFFF;
+        }
         double ws[TU];
 #pragma unroll
         for (int e = 0; e < TU; ++e) {
             int rank = 0;
+            if (rk && e < Tb) {
 #pragma unroll
-            for (int f = 0; f < TU; ++f) rank += iv[f] < iv[e] ? 1 : 0;
+                for (int f = 0; f < TU; ++f)
+                    if (f < Tb) rank += iv[f] < iv[e] ? 1 : 0;
+            }
             ws[e] = (e < T && (all_k || rank < need)) ? 1.0 : 0.0;
         }
 #pragma unroll
-        for (int e0 = 0; e0 < TU; e0 += 4) {
-            if (e0 >= T) break;
-            double f[4][FW];
+        // two entries a round, their loads together; rounds past the wave's last entry skipped
+        for (int e0 = 0; e0 < TU; e0 += 2) {
+            if (e0 < Tb) {
+                double f[2][FW];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const GLOBAL_AS double *fp = P.fs + (size_t)pe[e0 + u] * FW;
+                for (int u = 0; u < 2; ++u) {
+                    const GLOBAL_AS double *fp = P.fs + (size_t)pe[e0 + u] * FW;
 #pragma unroll
-                for (int bd = 0; bd < FW; ++bd) f[u][bd] = fp[bd];
-            }
+                    for (int bd = 0; bd < FW; ++bd) f[u][bd] = fp[bd];
+                }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < 2; ++u) {
 #pragma unroll
-                for (int bd = 0; bd < FW; ++bd) cs[bd] = fma(f[u][bd], ws[e0 + u], cs[bd]);
+                    for (int bd = 0; bd < FW; ++bd) cs[bd] = fma(f[u][bd], ws[e0 + u], cs[bd]);
+                }
             }
         }
     }
