@@ -92,8 +92,11 @@ def unpack_rows(r):
     [n_pix][mask_words] for a batch fetch (ccdgpu_fetch_batch_rows)."""
     n_pix, n_obs, n = r.n_pix, r.n_obs, r.n_rows
     off = np.ctypeslib.as_array(r.row_offsets, shape=(n_pix + 1,)).copy()
-    rows = np.frombuffer(ctypes.string_at(ctypes.cast(r.rows, ctypes.c_void_p), n * ROW_DTYPE.itemsize),
-                         dtype=ROW_DTYPE).copy() if n else np.zeros(0, ROW_DTYPE)
+    # one numpy copy straight out of library memory (numpy releases the GIL for it: the tile
+    # runner's worker threads keep issuing uploads meanwhile); no intermediate bytes object
+    rows = (np.ctypeslib.as_array(ctypes.cast(r.rows, ctypes.POINTER(ctypes.c_uint8)),
+                                  shape=(n * ROW_DTYPE.itemsize,)).view(ROW_DTYPE).copy()
+            if n else np.zeros(0, ROW_DTYPE))
     if bool(r.mask_bits):
         w = r.mask_words
         bits = np.ctypeslib.as_array(r.mask_bits, shape=(max(n_pix * w, 1),))[:n_pix * w].reshape(n_pix, w).copy()

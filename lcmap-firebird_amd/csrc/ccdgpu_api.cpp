@@ -61,6 +61,30 @@ struct DevBuf {
     }
 };
 
+// Page-locked host staging (hipHostMalloc), grown on demand: device-to-host copies into it run as
+// one DMA at link speed instead of the runtime's chunked bounce through its own pinned buffers.
+struct PinBuf {
+    unsigned char *p = nullptr;
+    size_t cap = 0;  // bytes
+    int ensure(size_t n) {
+        if (n <= cap && p) return 0;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        if (hipHostMalloc(reinterpret_cast<void **>(&p), n ? n : 1, hipHostMallocDefault) != hipSuccess) {
+            p = nullptr;
+            return fail(CCDGPU_ENOMEM, "hipHostMalloc failed (" + std::to_string(n) + " bytes)");
+        }
+        cap = n;
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
 double chi2_5_cdf(double x) {
     if (x <= 0) return 0.0;
     return std::erf(std::sqrt(x / 2.0)) - std::sqrt(2.0 * x / M_PI) * std::exp(-x / 2.0) * (1.0 + x / 3.0);
@@ -169,6 +193,7 @@ struct ccdgpu_ctx {
     DevBuf<int64_t> row_off, seg_off1;
     DevBuf<int32_t> row_xy;     // per-chip (cx, cy) of a batch row fetch
     DevBuf<int8_t> mask8;
+    PinBuf h_rows;              // pinned landing zone of a batch row fetch (rows, then mask words)
     DevBuf<int64_t> slot_dates[CCDGPU_UPLOAD_SLOTS];   // upload slots (ccdgpu_stage_slot / ccdgpu_run_slot)
     DevBuf<int16_t> slot_spectra[CCDGPU_UPLOAD_SLOTS];
     DevBuf<uint16_t> slot_qa[CCDGPU_UPLOAD_SLOTS];
@@ -205,6 +230,7 @@ struct ccdgpu_ctx {
         if (copy_stream) (void)hipStreamDestroy(copy_stream);
         rows.release();
         mask8.release();
+        h_rows.release();
         for (auto &e : ev)
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
@@ -773,12 +799,26 @@ static int fetch_rows_range(ccdgpu_ctx *c, int32_t c0, int32_t c1, const int32_t
         return fail(CCDGPU_ENOMEM, "host allocation failed");
     }
     std::memcpy(out->row_offsets, roff.data(), sizeof(int64_t) * (np + 1));
-    HIPCHK(hipMemcpyAsync(out->rows, c->rows.p, sizeof(ccdgpu_row) * (size_t)n_rows, hipMemcpyDeviceToHost, c->stream));
-    if (packed_mask)
-        HIPCHK(hipMemcpyAsync(out->mask_bits, c->mask.p + (size_t)p0 * c->mask_words, sizeof(uint32_t) * nbits,
+    const size_t row_bytes = sizeof(ccdgpu_row) * (size_t)n_rows;
+    if (packed_mask) {
+        // batch fetch: rows and mask words land in the context's pinned buffer by DMA (one copy
+        // each at link speed), then go to the caller's buffers with a host memcpy
+        const size_t bit_bytes = sizeof(uint32_t) * nbits;
+        const size_t bit_at = (row_bytes + 255) & ~(size_t)255;
+        if ((rc = c->h_rows.ensure(bit_at + bit_bytes))) {
+            ccdgpu_rows_free(out);
+            return rc;
+        }
+        HIPCHK(hipMemcpyAsync(c->h_rows.p, c->rows.p, row_bytes, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(c->h_rows.p + bit_at, c->mask.p + (size_t)p0 * c->mask_words, bit_bytes,
                               hipMemcpyDeviceToHost, c->stream));
-    else
-        HIPCHK(hipMemcpyAsync(out->mask, c->mask8.p, (size_t)nd, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        std::memcpy(out->rows, c->h_rows.p, row_bytes);
+        std::memcpy(out->mask_bits, c->h_rows.p + bit_at, bit_bytes);
+        return 0;
+    }
+    HIPCHK(hipMemcpyAsync(out->rows, c->rows.p, row_bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(out->mask, c->mask8.p, (size_t)nd, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
 }
