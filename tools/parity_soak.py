@@ -3,7 +3,7 @@ batch per config, ccdgpu_stage_chips) against the C restatement oracle on the sa
 the test suite's parity bar (tests/parity_util.py: every integer / index output exact, floats
 within 1e-6 relative).  Chips are spread over the synthetic tile so both cadences (base 1421 obs,
 sidelap 2121 obs) are covered.  Prints one JSON summary.
-Usage: python tools/parity_soak.py [C3 chips] [C5 chips] [oracle threads]"""
+Usage: python tools/parity_soak.py [C3 chips] [C5 chips] [oracle threads] [C2 chips] [C4 chips]"""
 import json
 import os
 import sys
@@ -51,10 +51,12 @@ def main():
     n3 = int(sys.argv[1]) if len(sys.argv) > 1 else 12
     n5 = int(sys.argv[2]) if len(sys.argv) > 2 else 4
     threads = int(sys.argv[3]) if len(sys.argv) > 3 else 16
+    n2 = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+    n4 = int(sys.argv[5]) if len(sys.argv) > 5 else 0
     ctx = ccdgpu.Context(0)
     res = {'tool': 'tools/parity_soak.py', 'library': ccdgpu.LIB_PATH, 'bar': 'tests/parity_util.py (ints exact, '
            'floats 1e-6 rel)', 'oracle': 'oracle/ccd_oracle.c (C restatement), %d threads' % threads,
-           'runs': [soak(3, n3, threads, ctx)] + ([soak(5, n5, threads, ctx)] if n5 else [])}
+           'runs': [soak(w, n, threads, ctx) for w, n in ((3, n3), (5, n5), (2, n2), (4, n4)) if n]}
     ctx.close()
     res['pixels'] = sum(r['pixels'] for r in res['runs'])
     res['mismatched_pixels'] = sum(r['mismatched_pixels'] for r in res['runs'])
