@@ -1,30 +1,35 @@
 #!/usr/bin/env python3
 """bench.py -- pixels/s change-detected on MI355X (BASELINE.json metric), one JSON line.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--chips B] [--config C]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload (BASELINE.json configs[2], the CONUS ARD tile the metric names):
-chips of a 5000x5000-pixel tile (2500 chips of 100x100 pixels, Landsat 4-8 1982-2017 cadence,
-synthetic ARD from libccdsynth).  Rank r (one process per GPU) owns B chips spread evenly over
-the tile -- the tile's own mix of base-cadence (1421 obs) and sidelap (2121 obs) chips, about
-half each -- staged in HBM as ONE ragged batch (ccdgpu_stage_chips).  A "step" is one
-pass of the full detection hot path over those B chips: per-chip date sort + design rows, the
-per-pixel pyccd state machine, the per-pixel segment-count scan and the segment CSR scatter,
-results left in HBM.  Chips are independent: no data-path collective, weak scaling (fixed chips
-per GPU).  The timed region is bracketed by a barrier and a device synchronize on both sides;
-the reported time is the max over ranks.  --config 2/4/5 selects the other synthetic configs
-(C2 1000-obs chips, C4 high-cloud/snow, C5 change-dense) over the same chip ids.
+Headline (``value``; SURVEY.md §8(d): P / wall time including H2D and the D2H of the packed
+results; BASELINE.json configs[2], the CONUS ARD tile the metric names): every rank (one process
+per GPU) change-detects one full 5000x5000-pixel tile -- 2500 DISTINCT chips of 100x100 pixels,
+Landsat 4-8 1982-2017 cadence, the tile's own base-cadence (1421 obs) / sidelap (2121 obs) mix
+-- through the product tile driver ``ccdc.runner.changedetection`` (reference
+core.changedetection, ccdc/core.py:78-123): a dynamic chip queue shared by all ranks, two
+contexts per GPU, pinned host batches uploaded while the previous batch is detected, rows packed
+on the device and fetched back, per-chip summaries gathered on rank 0.  Chip ARD comes from the
+device generator (ccdgpu.synth.TileSource): each batch is generated on the GPU and copied into
+pinned host memory before the runner uploads it, so every chip is distinct and reaches the
+detection path through host memory and PCIe like fetched ARD (its GPU time and device-to-host
+copy are NOT excluded: the headline is pessimistic by that much).  A "step" = 1/K of the tile
+(ceil(2500 / K) chips per rank); the K steps are timed as one changedetection call bracketed by
+a barrier and a device synchronize; W warmup steps run first on chips of another tile.  Weak
+scaling: one tile per GPU (rank r's tile = chips 2500 r .. 2500 r + 2499 of the generator).
 
-value = total pixels of all ranks / time (inputs resident in HBM).  roofline = counted FP64
-flops of the detection kernel per launch / its duration vs the MI355X FP64 vector peak
-(78.6 TFLOP/s; the path is FP64 vector ALU, not a GEMM).  value_e2e = the PCIe-inclusive rate of
-the streaming leg (pinned uploads overlapped with detection, device-packed rows fetched back).
+``resident``: the detection hot path alone with inputs resident in HBM (64 tile chips per GPU,
+one ragged batch per step, K steps), the kernel behind the ``roofline`` (counted FP64 flops per
+launch / the launch's duration vs the MI355X FP64 vector peak, 78.6 TFLOP/s: the path is FP64
+vector ALU, not a GEMM).  --config 2/4/5 selects the other synthetic configs for both legs.
 cpu_baseline = the C restatement oracle (oracle/libccdoracle.so, "port") on a bounded sample of
-the same chips, on this host's cores; cpu_baseline_pyccd_restatement = the pyccd-structured numpy
-restatement (oracle/ccd_ref.py) under multiprocessing.Pool on a fixed sample -- the stand-in
-for the reference's per-pixel ccd.detect (ccdc/pyccd.py:168), which is not installable here.
+the same chips on this host's cores (the box's 16-thread share of one GPU; the same on every
+affinity CPU as cpu_baseline_all_cores); cpu_baseline_pyccd_restatement = the pyccd-structured
+numpy restatement (oracle/ccd_ref.py) under multiprocessing.Pool on a fixed sample -- the
+stand-in for the reference's per-pixel ccd.detect (ccdc/pyccd.py:168), not installable here.
 """
 import argparse
 import json
@@ -63,10 +68,7 @@ def parse():
                     help='pixels of the pyccd-structured restatement baseline sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-packer', action='store_true', help='skip the chip-packer (chipmunk decode) leg')
-    ap.add_argument('--no-stream', action='store_true', help='skip the end-to-end (PCIe-inclusive) streaming leg')
-    ap.add_argument('--stream-chips', type=int, default=16, help='chips per batch of the streaming leg')
-    ap.add_argument('--no-tile', action='store_true', help='skip the full-tile leg (ccdc.runner over 2500 chips)')
-    ap.add_argument('--tile-chips', type=int, default=TILE_CHIPS, help='chips of the tile leg (all ranks together)')
+    ap.add_argument('--tile-chips', type=int, default=TILE_CHIPS, help='chips of the headline tile leg per rank')
     ap.add_argument('--tile-batch', type=int, default=8, help='chips per launch in the tile leg')
     ap.add_argument('--tile-contexts', type=int, default=2, help='contexts per GPU in the tile leg')
     ap.add_argument('--tile-depth', type=int, default=2, help='batches each tile-leg context keeps uploaded ahead')
@@ -154,14 +156,76 @@ def main():
     from ccdgpu import synth
 
     cfg = synth.config(args.config)
-    ids = chip_ids(rank, args.chips, world, lambda c: synth.dates(cfg, c).shape[0])
-    batch = build_batch(cfg, ids)
-
     ndev = ccdgpu.device_count()
     if local >= ndev and not args.share_device:
         raise SystemExit('LOCAL_RANK %d but only %d device(s) visible' % (local, ndev))
     device = local % ndev
     n_devices = min(world, ndev) if args.share_device else world
+
+    res = resident_leg(args, cfg, rank, world, device, dist)
+    tl = tile_leg(args, cfg, rank, world, device, dist)
+    if rank == 0:
+        out = {
+            'metric': 'pixels/sec change-detected (CONUS ARD tile) at 1/2/4/8 MI355X; FP64 VALU %',
+            'value': tl['value'],
+            'unit': 'pixels/s',
+            'n_gpus': n_devices,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': tl['ms_per_step'],
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'f64',
+            'data': 'synthetic (Landsat 4-8 ARD, seeded; tile leg: every chip distinct, generated on the GPU into pinned host memory)',
+            'config': {
+                'workload': '%s; one full 5000x5000-pixel tile per GPU (%d distinct 100x100-pixel chips per rank, %s), '
+                            'PCIe-inclusive: chips uploaded from pinned host memory, detected, segment/pixel rows packed '
+                            'on the device and fetched back, per-chip summaries gathered on rank 0 (ccdc.runner.changedetection); '
+                            'a step = %d chips per rank' % (
+                                CONFIG_NAMES[args.config], tl['chips_per_rank'],
+                                ', '.join('%d chips of %d obs' % (v, k) for k, v in sorted(tl['n_obs_mix'].items())),
+                                tl['chips_per_step']),
+                'workload_key': 'tile%d_config%d_chips%d_pcie' % (args.tile_chips, args.config, tl['chips_per_rank']),
+                'synthetic_config': args.config,
+                'chips_per_gpu': tl['chips_per_rank'],
+                'pixels_per_chip': PIXELS_PER_CHIP,
+                'n_obs_mix': tl['n_obs_mix'],
+                'tile_chips': TILE_CHIPS,
+                'ranks': world,
+                'parallelism': 'chip-sharded x%d (one process per GPU, shared dynamic chip queue, no collective)' % world,
+            },
+            'roofline': res['roofline'],
+            'value_resident': res['value'],
+            'resident': res,
+            'tile': tl,
+        }
+        if not args.no_packer:
+            ctx = ccdgpu.Context(device)
+            out['chip_packer'] = packer_leg(ctx, res['batch'])
+            ctx.close()
+        if world == 1 and not args.no_cpu_baseline:
+            d, s, q = res['batch'].chip(0)
+            out['cpu_baseline'] = cpu_baseline(res['batch'], args)
+            out['speedup_vs_cpu_baseline'] = out['value'] / out['cpu_baseline']['value']
+            out['cpu_baseline_all_cores'] = cpu_baseline(res['batch'], args, all_cores=True)
+            out['speedup_vs_cpu_baseline_all_cores'] = out['value'] / out['cpu_baseline_all_cores']['value']
+            out['cpu_baseline_pyccd_restatement'] = restatement_baseline(d, s, q, args)
+            out['speedup_vs_pyccd_restatement'] = out['value'] / out['cpu_baseline_pyccd_restatement']['value']
+        res.pop('batch')
+        print(json.dumps(out), file=json_out, flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def resident_leg(args, cfg, rank, world, device, dist):
+    """The detection hot path alone, inputs resident in HBM: the rank's ``--chips`` tile chips
+    (the tile's cadence mix, spread over the tile) staged once as ONE ragged batch; K steps of
+    prep + detect + scan + scatter, two contexts alternating so a launch overlaps the previous
+    one's tail.  Behind the roofline."""
+    import ccdgpu
+    ids = chip_ids(rank, args.chips, world, lambda c: synth_nobs(cfg, c))
+    batch = build_batch(cfg, ids)
     ctxs = [ccdgpu.Context(device) for _ in range(max(1, args.contexts))]
     for c in ctxs:
         c.stage_chips(batch)
@@ -204,14 +268,10 @@ def main():
     ctx.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    pixels_total = world * batch.total_pixels * args.steps
-    value = pixels_total / elapsed
+    elapsed = max_over_ranks(elapsed, dist)
+    for c in ctxs:
+        c.close()
+    value = world * batch.total_pixels * args.steps / elapsed
     det_avg = float(np.mean(det_ms))
     dev_avg = float(np.mean(dev_ms))
     # per-launch time behind the roofline: the HIP-event launch duration on the launching stream;
@@ -230,34 +290,14 @@ def main():
                 traffic = pmc.get('hbm_bytes_per_launch')
         except Exception:
             traffic = None
-
-    out = {
-        'metric': 'pixels/sec change-detected (CONUS ARD tile) at 1/2/4/8 MI355X; FP64 VALU %',
-        'value': value,
-        'unit': 'pixels/s',
-        'n_gpus': n_devices,
-        'steps': args.steps,
-        'warmup': args.warmup,
-        'ms_per_step': elapsed / args.steps * 1e3,
-        'higher_is_better': True,
-        'scaling': 'weak',
-        'vs_baseline': None,
-        'dtype': 'f64',
-        'data': 'synthetic (libccdsynth Landsat 4-8 ARD chips, seeded)',
-        'config': {
-            'workload': '%s; %d tile chips per GPU spread evenly over the tile (chip %d, %d, ..., %d; %s), one ragged batch per step, inputs resident in HBM' % (
-                CONFIG_NAMES[args.config], len(ids), ids[0], ids[1] if len(ids) > 1 else ids[0], ids[-1],
-                ', '.join('%d chips of %d obs' % (v, k) for k, v in sorted(mix.items()))),
-            'workload_key': workload_key,
-            'synthetic_config': args.config,
-            'chips_per_gpu': len(ids), 'contexts_per_gpu': len(ctxs),
-            'pixels_per_chip': PIXELS_PER_CHIP,
-            'n_obs_mix': mix,
-            'mean_n_obs': float(np.mean(batch.n_obs)),
-            'tile_chips': TILE_CHIPS,
-            'ranks': world,
-            'parallelism': 'chip-sharded x%d (one process per GPU, no collective)' % world,
-        },
+    return {
+        'value': value, 'unit': 'pixels/s', 'steps': args.steps, 'ms_per_step': elapsed / args.steps * 1e3,
+        'workload': '%s; %d tile chips per GPU spread evenly over the tile (chip %d, %d, ..., %d; %s), one ragged batch '
+                    'per step, inputs resident in HBM' % (
+                        CONFIG_NAMES[args.config], len(ids), ids[0], ids[1] if len(ids) > 1 else ids[0], ids[-1],
+                        ', '.join('%d chips of %d obs' % (v, k) for k, v in sorted(mix.items()))),
+        'workload_key': workload_key, 'chips_per_gpu': len(ids), 'contexts_per_gpu': len(ctxs), 'n_obs_mix': mix,
+        'mean_n_obs': float(np.mean(batch.n_obs)),
         'roofline': {
             'bound': 'fp64-valu',
             'achieved': achieved_tf,
@@ -267,6 +307,7 @@ def main():
             'traffic': traffic,
             'kernel': {'w1': 'ccd_detect', 'w2': 'ccd_detect_w2', 'w4': 'ccd_detect_w4'}.get(
                 os.environ.get('CCDGPU_KERNEL', 'w3'), 'ccd_detect_w3'),
+            'workload_key': workload_key,
             'traffic_note': 'traffic = HBM bytes per launch from rocprofv3 --pmc (profiles/pmc_detect.json, same workload_key), else null',
             'kernel_ms_per_launch': launch_ms,
             'kernel_ms_hip_events': det_avg,
@@ -279,76 +320,111 @@ def main():
         },
         'segments_per_step': segs * world,
         'prep_ms_per_launch': float(np.mean(prep_ms)),
+        'batch': batch,
     }
 
-    if not args.no_tile:
-        # every rank takes part (shared dynamic queue); rank 0 gets the gathered result
-        tl = tile_leg(args, cfg, rank, world, device, dist)
-        if rank == 0:
-            out['tile'] = tl
-            out['value_e2e'] = tl['value']
-    if rank == 0 and not args.no_stream:
-        out['end_to_end'] = stream_leg(ctx, batch, min(args.stream_chips, batch.n_chips))
-        out.setdefault('value_e2e', out['end_to_end']['overlapped_pinned'])
-    if rank == 0 and not args.no_packer:
-        out['chip_packer'] = packer_leg(ctx, batch)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        d, s, q = batch.chip(0)
-        out['cpu_baseline'] = cpu_baseline(d, s, q, args)
-        out['speedup_vs_cpu_baseline'] = value / out['cpu_baseline']['value']
-        out['cpu_baseline_pyccd_restatement'] = restatement_baseline(d, s, q, args)
-        out['speedup_vs_pyccd_restatement'] = value / out['cpu_baseline_pyccd_restatement']['value']
-    if rank == 0:
-        print(json.dumps(out), file=json_out, flush=True)
-    for c in ctxs:
-        c.close()
-    if dist is not None:
-        dist.destroy_process_group()
+
+def max_over_ranks(x, dist):
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+class _KeptContext(object):
+    """A context created before the timed region and lent to the runner (whose close() at the
+    end of a tile would otherwise free it): the timed run measures the steady-state pipeline, not
+    context creation."""
+
+    def __init__(self, ctx):
+        self._ctx = ctx
+
+    def __getattr__(self, name):
+        return getattr(self._ctx, name)
+
+    def close(self):
+        pass
 
 
 def tile_leg(args, cfg, rank, world, device, dist):
-    """The product tile driver (ccdc.runner.changedetection; reference core.changedetection,
-    ccdc/core.py:78-123) over the tile's chip grid on every rank's GPU: one dynamic chip queue
-    shared by all ranks (the process group's store), two contexts per GPU each keeping two pinned
-    batch uploads queued ahead of its detection, device row packing, rows fetched back per batch, per-chip
-    summaries gathered on rank 0.  PCIe-inclusive.  Chip ARD comes from a pool of two
-    pre-generated pinned batches of the tile's cadence mix, cycled over the tile positions, so
-    host-side synthetic generation (the chipmunk fetch stand-in) stays out of the timing."""
+    """The headline: ``--tile-chips`` distinct chips per rank (default one full 2500-chip tile)
+    through ccdc.runner.changedetection with chips generated on the GPU into pinned host memory
+    (ccdgpu.synth.TileSource).  Positions 0 .. world * tile_chips - 1 share one dynamic queue;
+    position p is generator chip p (tile p // 2500, chip p % 2500 of it; coordinates on the
+    reference grid of test/data/tile_response.json shifted one tile width per tile).  W warmup
+    steps run first on chips of a separate tile range (positions offset by 10^6)."""
+    import ccdgpu
     from ccdc import runner
+    from ccdgpu import synth
     B = args.tile_batch
-    ids = chip_ids(0, 2 * B, 1, lambda c: synth_nobs(cfg, c))
-    pool = [build_batch(cfg, ids[k::2], pinned=True) for k in range(2)]
-    tails = {}
+    K = max(1, args.steps)
+    per_rank = int(args.tile_chips)
+    chips_per_step = -(-per_rank // K)
+    total = world * per_rank
+    warm_total = world * min(per_rank, args.warmup * chips_per_step)
+    src_timed = synth.TileSource(cfg, device=device, batch_chips=B, chip_of=lambda p: p)
+    src_warm = synth.TileSource(cfg, device=device, batch_chips=B, chip_of=lambda p: 1000000 + p)
+    pool = args.tile_contexts * (args.tile_depth + 1) + args.tile_contexts
+    src_timed.prefill(pool)
+    src_warm._free = src_timed._free  # one pinned pool for both phases
+    src_warm.allocated = src_timed.allocated
+    ctxs = [ccdgpu.Context(device) for _ in range(args.tile_contexts)]
+    lent = iter([])
 
-    def source(pos):
-        b = pool[(pos[0] // B) % 2]
-        if len(pos) == b.n_chips:
-            return b
-        if len(pos) not in tails:
-            tails[len(pos)] = prefix_batch(b, len(pos), True)
-        return tails[len(pos)]
+    def factory(dev):
+        return _KeptContext(next(lent))
 
-    xys = [(-1815585 + 3000 * (c // 50), 1064805 - 3000 * (c % 50)) for c in range(TILE_CHIPS)]
-    sink = runner.SummarySink(digest=False)
+    def xy(p):
+        t, c = divmod(p % 1000000, TILE_CHIPS)
+        return (-1815585 + 3000 * (c // 50) + 150000 * t, 1064805 - 3000 * (c % 50))
+
+    def run(n, src):
+        nonlocal lent
+        lent = iter(ctxs)
+        sink = runner.SummarySink(digest=False)
+        xys = [xy(p) for p in range(n)]
+        return runner.changedetection(xys, src, device=device, contexts=args.tile_contexts, batch_chips=B,
+                                      sink=sink, upload_depth=args.tile_depth, context_factory=factory)
+
+    if warm_total:
+        run(warm_total, src_warm)
     if dist is not None:
         dist.barrier()
+    ctxs[0].synchronize()
+    gen0 = src_timed.generate_seconds
     t = time.perf_counter()
-    res = runner.changedetection(xys, source, device=device, contexts=args.tile_contexts, batch_chips=B,
-                                 number=args.tile_chips, sink=sink, upload_depth=args.tile_depth)
-    el = time.perf_counter() - t
+    res = run(total, src_timed)
+    ctxs[0].synchronize()
+    if dist is not None:
+        dist.barrier()
+    el = max_over_ranks(time.perf_counter() - t, dist)
+    gen_s = src_timed.generate_seconds - gen0
+    for c in ctxs:
+        c.close()
+    src_timed.close()
+    src_warm.close()
     if res is None:
         return None
     px = sum(c['n_pix'] for c in res['chips'])
     mix = {}
     for c in res['chips']:
         mix[c['n_obs']] = mix.get(c['n_obs'], 0) + 1
-    return {'value': px / el, 'unit': 'pixels/s', 'seconds': el, 'chips': len(res['chips']), 'pixels': px,
-            'chips_per_launch': B, 'contexts_per_gpu': args.tile_contexts, 'upload_depth': args.tile_depth,
-            'ranks': world, 'n_obs_mix': mix,
+    ranks = {st['rank']: st for st in res['ranks']}
+    return {'value': px / el, 'unit': 'pixels/s', 'seconds': el, 'ms_per_step': el / K * 1e3, 'steps': K,
+            'chips_per_step': chips_per_step, 'chips_per_rank': per_rank, 'chips': len(res['chips']), 'pixels': px,
+            'distinct_chips': len(res['chips']), 'chips_per_launch': B, 'contexts_per_gpu': args.tile_contexts,
+            'upload_depth': args.tile_depth, 'ranks': world, 'n_obs_mix': mix,
             'rows': sum(c['rows'] for c in res['chips']),
-            'chips_per_rank': {st['rank']: st['chips'] for st in res['ranks']},
-            'worker_seconds_rank0': {k: round(v, 3) for k, v in res['ranks'][0].items() if k.endswith('_seconds')},
-            'note': 'ccdc.runner tile driver: shared dynamic chip queue, H2D of pinned ARD + detection + device row packing + D2H of rows + gather of per-chip summaries on rank 0; chip ARD cycled over 2 pre-generated pinned batches of the tile mix'}
+            'chips_per_rank_done': {r: st['chips'] for r, st in ranks.items()},
+            'tail_seconds_per_rank': {r: round(st.get('tail_seconds', 0.0), 3) for r, st in ranks.items()},
+            'generate_seconds_rank0': round(gen_s, 3),
+            'pinned_pool_batches': src_timed.allocated,
+            'worker_seconds_rank0': {k: round(v, 3) for k, v in ranks[0].items() if k.endswith('_seconds')},
+            'note': 'ccdc.runner tile driver over distinct device-generated chips: GPU generation + D2H into pinned '
+                    'host batches (not excluded), H2D upload overlapped with detection, device row packing, D2H of rows, '
+                    'gather of per-chip summaries on rank 0'}
 
 
 def synth_nobs(cfg, c):
@@ -364,38 +440,6 @@ def prefix_batch(batch, n, pinned):
     b.spectra[...] = batch.spectra[:b.spectra.shape[0]]
     b.qa[...] = batch.qa[:b.qa.shape[0]]
     return b
-
-
-def stream_leg(ctx, batch, n, batches=6):
-    """End-to-end rate (never ``value``): each batch = the first n chips of the workload (the
-    tile's cadence mix) uploaded, detected and their rows packed on the device and fetched back (the product
-    output: float32 segment rows + per-date pixel masks).  'sequential' runs upload -> detect ->
-    fetch one after another from pageable memory; 'overlapped' uploads batch i+1 from pinned
-    memory on the copy stream (ccdgpu_stage_slot_chips) while batch i is detected."""
-    pins = [prefix_batch(batch, n, True) for _ in range(2)]
-    page = prefix_batch(batch, n, False)
-    cx = np.arange(n, dtype=np.int32) * 3000
-    cy = np.zeros(n, dtype=np.int32)
-    px = page.total_pixels * batches
-    t = time.perf_counter()
-    for i in range(batches):
-        ctx.stage_chips(page)
-        ctx.run()
-        ctx.fetch_batch_rows(cx, cy)
-    seq = time.perf_counter() - t
-    t = time.perf_counter()
-    ctx.stage_slot_chips(0, pins[0])
-    for i in range(batches):
-        if i + 1 < batches:
-            ctx.stage_slot_chips((i + 1) & 1, pins[(i + 1) & 1])
-        ctx.run_slot(i & 1)
-        ctx.fetch_batch_rows(cx, cy)
-    ovl = time.perf_counter() - t
-    return {'unit': 'pixels/s', 'batches': batches, 'chips_per_batch': n,
-            'input_bytes_per_batch': int(page.nbytes), 'n_obs_mix': cadence_mix(page),
-            'sequential_pageable': px / seq, 'overlapped_pinned': px / ovl,
-            'h2d_gbs_overlapped': page.nbytes * batches / ovl / 1e9,
-            'note': 'H2D of the inputs + detection + device row packing + D2H of the rows; not the headline value'}
 
 
 def packer_leg(ctx, batch):
@@ -441,23 +485,45 @@ def host_cpus():
                  'omp_num_threads_share': share or None}
 
 
-def cpu_baseline(dates, S, Q, args):
-    """C restatement oracle (oracle/libccdoracle.so) on a bounded pixel sample of chip 0,
-    OpenMP over pixels on this host's cores."""
+def cpu_baseline(batch, args, all_cores=False):
+    """C restatement oracle (oracle/libccdoracle.so) on a bounded pixel sample of the workload's
+    chips that share chip 0's date vector, OpenMP over pixels: on the box's CPU share of one GPU
+    (OMP_NUM_THREADS), or with ``all_cores`` on every CPU this process may run on."""
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
     import oracle_ctypes
     thr, info = host_cpus()
-    n_probe = 32 * thr
+    if all_cores:
+        thr = info['affinity_cpus']
+    dates = batch.chip(0)[0]
+    same = [c for c in range(batch.n_chips) if np.array_equal(batch.chip(c)[0], dates)]
+
+    def sample(n):
+        """the first n pixels of the chips in `same`, as one (spectra, qa) pair"""
+        S, Q, got = [], [], 0
+        for c in same:
+            _, s, q = batch.chip(c)
+            k = min(n - got, s.shape[1])
+            S.append(s[:, :k])
+            Q.append(q[:k])
+            got += k
+            if got >= n:
+                break
+        return np.ascontiguousarray(np.concatenate(S, axis=1)), np.ascontiguousarray(np.concatenate(Q, axis=0))
+
+    n_probe = min(32 * thr, PIXELS_PER_CHIP * len(same))
+    S, Q = sample(n_probe)
     t = time.perf_counter()
-    oracle_ctypes.detect_batch(dates, S[:, :n_probe], Q[:n_probe], threads=thr)
+    oracle_ctypes.detect_batch(dates, S, Q, threads=thr)
     rate = n_probe / (time.perf_counter() - t)
-    n = int(min(PIXELS_PER_CHIP, max(n_probe, rate * args.cpu_seconds)))
+    secs = args.cpu_seconds if not all_cores else min(args.cpu_seconds, 5.0)
+    n = int(min(PIXELS_PER_CHIP * len(same), max(n_probe, rate * secs)))
+    S, Q = sample(n)
     t = time.perf_counter()
-    oracle_ctypes.detect_batch(dates, S[:, :n], Q[:n], threads=thr)
+    oracle_ctypes.detect_batch(dates, S, Q, threads=thr)
     el = time.perf_counter() - t
     out = {'value': n / el, 'unit': 'pixels/s', 'cores': thr, 'kind': 'port',
-           'sample': 'first %d pixels of chip 0 of the same workload (%d obs, %.1f s), C restatement oracle, OpenMP %d threads' % (
-               n, dates.shape[0], el, thr)}
+           'sample': 'first %d pixels of the workload chips sharing chip 0\'s %d dates (%.1f s), C restatement oracle, '
+                     'OpenMP %d threads%s' % (n, dates.shape[0], el, thr, ' (every affinity CPU)' if all_cores else '')}
     out.update(info)
     return out
 

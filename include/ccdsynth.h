@@ -38,6 +38,23 @@ int ccdsynth_dates(const ccdsynth_cfg *cfg, int32_t chip_index, int64_t *dates, 
 int ccdsynth_chip(const ccdsynth_cfg *cfg, int32_t chip_index, int32_t pix0, int32_t n_pix,
                   int32_t n_obs, const int64_t *dates, int16_t *spectra, uint16_t *qa);
 
+/* ---- device generator (lib/libccdsynth.so, csrc/ccd_synth.hip): the same samples computed on
+ * a gfx950 GPU and copied into host buffers (pinned for full PCIe rate), for inputs too large to
+ * generate on the host (a tile's 2500 distinct chips).  Same arithmetic as ccdsynth_chip
+ * (csrc/synth_core.h); see there for how close the two agree.  One handle per thread. */
+typedef struct ccdsynth_gpu ccdsynth_gpu;
+int ccdsynth_gpu_create(int device, ccdsynth_gpu **out);
+void ccdsynth_gpu_destroy(ccdsynth_gpu *g);
+/* last error of this thread's calls (static string) */
+const char *ccdsynth_gpu_error(void);
+/* n_chips chips: chip c is tile chip chip_ids[c] with pixels pix0[c] .. pix0[c]+n_pix[c]-1 and the
+ * n_obs[c] dates at dates + obs_off[c] (host, as ccdsynth_dates writes them).  Writes spectra
+ * [7][n_pix][n_obs] at spectra + 7 * data_off[c] and qa [n_pix][n_obs] at qa + data_off[c] (host
+ * buffers: the layout of a staged batch, ccdgpu_stage_chips).  Returns 0 when the copies are done. */
+int ccdsynth_gpu_batch(ccdsynth_gpu *g, const ccdsynth_cfg *cfg, int32_t n_chips, const int32_t *chip_ids,
+                       const int32_t *pix0, const int32_t *n_pix, const int32_t *n_obs, const int64_t *obs_off,
+                       const int64_t *data_off, const int64_t *dates, int16_t *spectra, uint16_t *qa);
+
 #ifdef __cplusplus
 }
 #endif

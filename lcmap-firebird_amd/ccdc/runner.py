@@ -43,6 +43,10 @@ class LocalQueue(object):
             self._next = min(self.total, a + int(n))
             return list(range(a, self._next))
 
+    def remaining(self):
+        with self._lock:
+            return self.total - self._next
+
 
 class StoreQueue(object):
     """Dynamic queue of tile positions shared by every rank of a torch.distributed job: one atomic
@@ -67,6 +71,9 @@ class StoreQueue(object):
         end = int(self.store.add(self.key, int(n)))
         a = end - int(n)
         return list(range(min(a, self.total), min(end, self.total)))
+
+    def remaining(self):
+        return max(0, self.total - int(self.store.add(self.key, 0)))
 
 
 # --------------------------------------------------------------------------- sinks
@@ -126,11 +133,20 @@ class ParquetSink(object):
 
 
 # --------------------------------------------------------------------------- the GPU worker
-def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, errors, depth=2):
+def _pull_size(queue, batch_chips, tail_chips):
+    """Chips to take next: a full batch, or a quarter batch once fewer than ``tail_chips``
+    positions remain, so the last chips of a tile spread over every worker of every rank
+    instead of waiting in one worker's upload queue."""
+    if tail_chips and batch_chips > 1 and hasattr(queue, 'remaining') and queue.remaining() < tail_chips:
+        return max(1, batch_chips // 4)
+    return batch_chips
+
+
+def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, errors, depth=2, tail_chips=0):
     """One context: up to ``depth`` batches uploaded (or uploading) ahead of the one being
     detected, one upload slot each, so the PCIe link stays busy while a batch is detected and
     its rows are fetched (with one batch ahead the link idles whenever both of a GPU's contexts
-    are past their upload)."""
+    are past their upload).  Near the end of the queue the batches shrink (``_pull_size``)."""
     try:
         clock = time.perf_counter
         free = list(range(depth + 1))
@@ -139,9 +155,11 @@ def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, er
         while True:
             while free and not exhausted:
                 t0 = clock()
-                pos = queue.next(batch_chips)
+                pos = queue.next(_pull_size(queue, batch_chips, tail_chips))
                 if not pos:
                     exhausted = True
+                    with stats['lock']:
+                        stats['queue_empty_at'] = max(stats['queue_empty_at'], t0 - stats['t0'])
                     break
                 batch = source(pos)
                 if batch.n_chips != len(pos):
@@ -173,6 +191,9 @@ def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, er
                 r0, r1 = int(off[p0]), int(off[p1])
                 d, _, _ = pbatch.chip(c)
                 sink(p, int(cx[c]), int(cy[c]), d, off[p0:p1 + 1] - r0, rows[r0:r1], pbatch.mask_bits_of(mask, c))
+            release = getattr(source, 'release', None)
+            if release is not None:
+                release(pbatch)  # its upload is done and its rows are out: the source may reuse it
             t5 = clock()
             with stats['lock']:
                 stats['batches'] += 1
@@ -187,30 +208,43 @@ def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, er
 
 
 def detect_tile(xys, source, queue, device=0, contexts=2, batch_chips=16, params=None, width=100,
-                sink=None, context_factory=None, upload_depth=2):
+                sink=None, context_factory=None, upload_depth=2, tail_chips=None):
     """Change detection of the tile chips at ``xys`` (list of (cx, cy), tile order) on one GPU.
 
     ``source(positions) -> ccdgpu.ChipBatch`` supplies the ARD of the chips at those tile
-    positions (pinned batches upload asynchronously); ``queue`` hands out positions (LocalQueue
+    positions (pinned batches upload asynchronously; a source with a ``release(batch)`` method
+    gets each batch back once its rows are fetched, to reuse its buffers); ``queue`` hands out positions (LocalQueue
     for one process, StoreQueue across ranks); ``sink(pos, cx, cy, dates, row_offsets, rows,
     mask_bits)`` receives each chip's device-packed rows and its processing masks as bit words
     [n_pix][words] (ccdgpu.abi.unpack_mask_bits; default sink: a SummarySink).  Returns the sink
     and this process's statistics.  ``upload_depth``: batches each context keeps uploaded or
-    uploading ahead of the one it detects (1 .. ccdgpu.UPLOAD_SLOTS - 1)."""
+    uploading ahead of the one it detects (1 .. ccdgpu.UPLOAD_SLOTS - 1).  ``tail_chips``: once
+    fewer positions than this remain in the queue, workers pull quarter batches (default: two
+    full batches per context of this process)."""
+    from ccdgpu import UPLOAD_SLOTS
+    if not 1 <= int(upload_depth) <= UPLOAD_SLOTS - 1:
+        raise ValueError('upload_depth must be in 1 .. %d (ccdgpu.UPLOAD_SLOTS - 1), got %r' % (UPLOAD_SLOTS - 1, upload_depth))
+    if int(batch_chips) < 1:
+        raise ValueError('batch_chips must be >= 1, got %r' % (batch_chips,))
+    if tail_chips is None:
+        tail_chips = 2 * int(batch_chips) * max(1, int(contexts))
     if context_factory is None:
         import ccdgpu
         context_factory = ccdgpu.Context
     sink = sink if sink is not None else SummarySink()
     # per-phase host seconds summed over the workers: source (ARD fetch), stage (upload call),
     # device (run_slot: waits for the upload, detects), fetch (row packing + D2H), sink
-    stats = {'lock': threading.Lock(), 'batches': 0, 'chips': 0, 'pixels': 0, 'rows': 0, 'device_seconds': 0.0,
-             'source_seconds': 0.0, 'stage_seconds': 0.0, 'fetch_seconds': 0.0, 'sink_seconds': 0.0}
+    # queue_empty_at: seconds from the start until a worker first found the queue empty (the
+    # rest of this process's time is its tail: the last batches draining)
+    t0 = time.perf_counter()
+    stats = {'lock': threading.Lock(), 't0': t0, 'batches': 0, 'chips': 0, 'pixels': 0, 'rows': 0, 'device_seconds': 0.0,
+             'source_seconds': 0.0, 'stage_seconds': 0.0, 'fetch_seconds': 0.0, 'sink_seconds': 0.0,
+             'queue_empty_at': 0.0}
     errors = []
     ctxs = [context_factory(device) for _ in range(max(1, int(contexts)))]
-    t0 = time.perf_counter()
     try:
-        th = [threading.Thread(target=_worker, args=(c, queue, source, xys, batch_chips, params, width, sink, stats, errors,
-                                                       max(1, int(upload_depth))))
+        th = [threading.Thread(target=_worker, args=(c, queue, source, xys, int(batch_chips), params, width, sink, stats,
+                                                       errors, int(upload_depth), int(tail_chips)))
               for c in ctxs]
         for t in th:
             t.start()
@@ -219,29 +253,49 @@ def detect_tile(xys, source, queue, device=0, contexts=2, batch_chips=16, params
     finally:
         for c in ctxs:
             c.close()
-    if errors:
-        raise errors[0]
     stats.pop('lock')
+    stats.pop('t0')
     stats['seconds'] = time.perf_counter() - t0
+    stats['tail_seconds'] = stats['seconds'] - stats['queue_empty_at'] if stats['queue_empty_at'] else 0.0
+    if errors:
+        errors[0].tile_stats = stats  # what this process did before the failure (changedetection's gather)
+        raise errors[0]
     return sink, stats
 
 
 _calls = [0]
+_gloo = {}  # one gloo group per default process group (created once, reused by every gather)
 
 
 def gather(obj, dist=None):
     """All ranks' ``obj`` as a list on rank 0 (None elsewhere); [obj] without a process group.
-    Uses a gloo group, so it works whatever backend the default group has."""
+    Uses a gloo group (created on first use and cached), so it works whatever backend the
+    default group has."""
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
         return [obj]
-    group = dist.new_group(backend='gloo')
+    from torch.distributed import distributed_c10d
+    key = id(distributed_c10d._get_default_group())
+    group = _gloo.get(key)
+    if group is None:
+        _gloo.clear()  # a group of an earlier (destroyed) default group is stale
+        group = _gloo[key] = dist.new_group(backend='gloo')
     out = [None] * dist.get_world_size() if dist.get_rank() == 0 else None
     dist.gather_object(obj, out, dst=0, group=group)
     return out
 
 
+class TileError(RuntimeError):
+    """A rank's worker failed during changedetection: raised on every rank after the gather, on
+    rank 0 with the first failing rank's error (``rank``, ``cause``)."""
+
+    def __init__(self, rank, cause):
+        super(TileError, self).__init__('rank %d: %s: %s' % (rank, type(cause).__name__, cause))
+        self.rank = rank
+        self.cause = cause
+
+
 def changedetection(tile, source, device=None, contexts=2, batch_chips=16, number=None, params=None,
-                    sink=None, width=100, context_factory=None, ctx=None, upload_depth=2):
+                    sink=None, width=100, context_factory=None, ctx=None, upload_depth=2, tail_chips=None):
     """Change detection for a tile on every GPU of the job (reference core.changedetection,
     ccdc/core.py:78-123).
 
@@ -250,7 +304,13 @@ def changedetection(tile, source, device=None, contexts=2, batch_chips=16, numbe
     ``source(positions) -> ChipBatch``.  Under torch.distributed every rank calls this with the
     same arguments: ranks share one dynamic chip queue and rank 0 gets the gathered result.
     Returns (on rank 0, else None) {'xys': processed chip coordinates in tile order, 'chips':
-    per-chip summaries, 'ranks': per-rank statistics}."""
+    per-chip summaries, 'ranks': per-rank statistics}.
+
+    A worker failure (QA error, device error, a failing source) does not strand the other
+    ranks: the failing rank still takes part in the gather, sending its error, and every rank
+    then raises -- rank 0 a ``TileError`` carrying the first failing rank's exception (its
+    ``cause``), the others their own error.  Without a process group the error propagates
+    unchanged."""
     try:
         import torch.distributed as dist
         dist_on = dist.is_available() and dist.is_initialized()
@@ -273,16 +333,32 @@ def changedetection(tile, source, device=None, contexts=2, batch_chips=16, numbe
         import os
         device = int(os.environ.get('LOCAL_RANK', '0'))
     log.info('change detection of %d chips, %d per launch, rank %d' % (len(xys), batch_chips, rank))
-    sink, stats = detect_tile(xys, source, queue, device=device, contexts=contexts, batch_chips=batch_chips,
-                              params=params, width=width, sink=sink, context_factory=context_factory,
-                              upload_depth=upload_depth)
+    error = None
+    try:
+        sink, stats = detect_tile(xys, source, queue, device=device, contexts=contexts, batch_chips=batch_chips,
+                                  params=params, width=width, sink=sink, context_factory=context_factory,
+                                  upload_depth=upload_depth, tail_chips=tail_chips)
+    except Exception as e:
+        if not (dist_on and dist.get_world_size() > 1):
+            raise
+        error = e
+        stats = dict(getattr(e, 'tile_stats', {}))
     stats['rank'] = rank
-    chip_summaries = getattr(sink, 'chips', [])
-    parts = gather((stats, chip_summaries), dist if dist_on else None)
+    chip_summaries = getattr(sink, 'chips', []) if error is None else []
+    err_msg = None if error is None else (type(error).__name__, str(error))
+    parts = gather((stats, chip_summaries, err_msg), dist if dist_on else None)
+    if error is not None:
+        if rank == 0:
+            raise TileError(0, error)
+        raise error
     if parts is None:
         return None
-    summaries = sorted((s for _, cs in parts for s in cs), key=lambda s: s['pos'])
+    failed = [(st.get('rank', r), e) for r, (st, _, e) in enumerate(parts) if e is not None]
+    if failed:
+        r, (name, msg) = failed[0]
+        raise TileError(r, RuntimeError('%s: %s' % (name, msg)))
+    summaries = sorted((s for _, cs, _ in parts for s in cs), key=lambda s: s['pos'])
     done = [s['pos'] for s in summaries]
     if done != list(range(len(xys))):
         raise RuntimeError('tile incomplete: %d of %d chips processed' % (len(set(done)), len(xys)))
-    return {'xys': tuple(xys[p] for p in done), 'chips': summaries, 'ranks': [st for st, _ in parts]}
+    return {'xys': tuple(xys[p] for p in done), 'chips': summaries, 'ranks': [st for st, _, _ in parts]}

@@ -132,7 +132,10 @@ class ChipBatch(object):
         d, s, q = b.chip(1)      # views: dates [n], spectra [7][n_pix][n], qa [n_pix][n]
     """
 
-    def __init__(self, n_pix, n_obs, pinned=False):
+    def __init__(self, n_pix, n_obs, pinned=False, storage=None):
+        """``storage``: (dates int64, spectra int16, qa uint16) 1-D arrays of at least the batch's
+        sizes (e.g. ``batch_storage``, reused across batches): the batch's arrays are their
+        prefixes instead of new allocations."""
         self.n_pix = np.ascontiguousarray(n_pix, dtype=np.int32).reshape(-1)
         self.n_obs = np.ascontiguousarray(n_obs, dtype=np.int32).reshape(-1)
         if self.n_pix.shape != self.n_obs.shape or self.n_pix.size == 0:
@@ -140,10 +143,19 @@ class ChipBatch(object):
         self.obs_off = np.concatenate([[0], np.cumsum(self.n_obs, dtype=np.int64)])
         self.pix_off = np.concatenate([[0], np.cumsum(self.n_pix, dtype=np.int64)])
         self.data_off = np.concatenate([[0], np.cumsum(self.n_pix.astype(np.int64) * self.n_obs)])
+        nd, ns = int(self.obs_off[-1]), int(self.data_off[-1])
+        self.storage = storage
+        if storage is not None:
+            sd, ss, sq = storage
+            if sd.dtype != np.int64 or ss.dtype != np.int16 or sq.dtype != np.uint16 or \
+                    sd.size < nd or ss.size < 7 * ns or sq.size < ns:
+                raise ValueError('storage too small or of the wrong types for this batch')
+            self.dates, self.spectra, self.qa = sd[:nd], ss[:7 * ns], sq[:ns]
+            return
         alloc = pinned_empty if pinned else np.empty
-        self.dates = alloc((int(self.obs_off[-1]),), np.int64)
-        self.spectra = alloc((7 * int(self.data_off[-1]),), np.int16)
-        self.qa = alloc((int(self.data_off[-1]),), np.uint16)
+        self.dates = alloc((nd,), np.int64)
+        self.spectra = alloc((7 * ns,), np.int16)
+        self.qa = alloc((ns,), np.uint16)
 
     @property
     def n_chips(self):
@@ -414,6 +426,14 @@ class _Pinned(object):
                 lib().ccdgpu_host_free(self.ptr)
         except Exception:
             pass
+
+
+def batch_storage(max_chips, max_pix, max_obs, pinned=True):
+    """Reusable buffers for ChipBatch(..., storage=...): room for ``max_chips`` chips of up to
+    ``max_pix`` pixels x ``max_obs`` observations."""
+    alloc = pinned_empty if pinned else np.empty
+    n = int(max_chips) * int(max_pix) * int(max_obs)
+    return (alloc((int(max_chips) * int(max_obs),), np.int64), alloc((7 * n,), np.int16), alloc((n,), np.uint16))
 
 
 def pinned_empty(shape, dtype):

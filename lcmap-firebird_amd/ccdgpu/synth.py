@@ -36,6 +36,10 @@ def lib():
         L.ccdsynth_chip.argtypes = [ctypes.POINTER(SynthCfg), ctypes.c_int32, ctypes.c_int32,
                                     ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_void_p]
+        L.ccdsynth_gpu_create.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+        L.ccdsynth_gpu_destroy.argtypes = [ctypes.c_void_p]
+        L.ccdsynth_gpu_error.restype = ctypes.c_char_p
+        L.ccdsynth_gpu_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(SynthCfg), ctypes.c_int32] + [ctypes.c_void_p] * 10
         _lib = L
     return _lib
 
@@ -76,3 +80,130 @@ def chip(cfg, chip_index, pix0=0, n_pix=10000, chip_dates=None, out=None):
     lib().ccdsynth_chip(ctypes.byref(cfg), int(chip_index), int(pix0), int(n_pix), int(n),
                         d.ctypes.data, spectra.ctypes.data, qa.ctypes.data)
     return d, spectra, qa
+
+
+class DeviceGenerator(object):
+    """The generator on a GPU (ccdsynth_gpu_*, csrc/ccd_synth.hip): the same samples as ``chip``
+    for whole batches of chips, computed in HBM and copied into a ``ccdgpu.ChipBatch`` (pinned for
+    full PCIe rate).  For inputs too large to generate on the host, e.g. a tile's 2500 distinct
+    chips.  Not thread-safe: one generator per thread."""
+
+    def __init__(self, device=0):
+        self._g = ctypes.c_void_p()
+        if lib().ccdsynth_gpu_create(int(device), ctypes.byref(self._g)) != 0:
+            raise RuntimeError('ccdsynth_gpu_create: %s' % lib().ccdsynth_gpu_error().decode())
+        self._dates = {}
+
+    def close(self):
+        if self._g:
+            lib().ccdsynth_gpu_destroy(self._g)
+            self._g = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def dates(self, cfg, c):
+        key = (bytes(cfg), int(c))
+        d = self._dates.get(key)
+        if d is None:
+            d = self._dates[key] = dates(cfg, c)
+        return d
+
+    def batch(self, cfg, chip_ids, n_pix=10000, pix0=0, out=None, pinned=True):
+        """Chips ``chip_ids`` (pixels pix0 .. pix0+n_pix-1 of each) as a ChipBatch: ``out`` when
+        given (its chip shapes must match), else a new one."""
+        import ccdgpu
+        ids = [int(c) for c in chip_ids]
+        nobs = [self.dates(cfg, c).shape[0] for c in ids]
+        if out is None:
+            out = ccdgpu.ChipBatch([n_pix] * len(ids), nobs, pinned=pinned)
+        elif list(out.n_obs) != nobs or list(out.n_pix) != [n_pix] * len(ids):
+            raise ValueError('out batch does not match the chips %s' % (ids,))
+        for j, c in enumerate(ids):
+            out.dates[out.obs_off[j]:out.obs_off[j + 1]] = self.dates(cfg, c)
+        a32 = lambda v: np.ascontiguousarray(v, dtype=np.int32)
+        cid, p0, npx, nob = a32(ids), a32([pix0] * len(ids)), a32(out.n_pix), a32(out.n_obs)
+        oo, do = np.ascontiguousarray(out.obs_off[:-1]), np.ascontiguousarray(out.data_off[:-1])
+        rc = lib().ccdsynth_gpu_batch(self._g, ctypes.byref(cfg), len(ids), cid.ctypes.data, p0.ctypes.data,
+                                      npx.ctypes.data, nob.ctypes.data, oo.ctypes.data, do.ctypes.data,
+                                      out.dates.ctypes.data, out.spectra.ctypes.data, out.qa.ctypes.data)
+        if rc != 0:
+            raise RuntimeError('ccdsynth_gpu_batch: %s' % lib().ccdsynth_gpu_error().decode())
+        return out
+
+
+class TileSource(object):
+    """``source(positions) -> ChipBatch`` for ccdc.runner: the tile chips at those positions, every
+    one distinct (chip id = tile position), generated on the GPU (DeviceGenerator, one per
+    calling thread) into pinned buffers from a pool, so they reach the detection path through
+    host memory and PCIe as fetched ARD would.  The runner hands each batch back with
+    ``release(batch)`` once its rows are fetched; the pool grows when every buffer is in use.
+    ``generate_seconds`` sums the time spent generating (GPU kernel + device-to-host copy)."""
+
+    def __init__(self, cfg, device=0, batch_chips=8, n_pix=10000, chip_of=None):
+        import threading
+        self.cfg = cfg
+        self.device = int(device)
+        self.batch_chips = int(batch_chips)
+        self.n_pix = int(n_pix)
+        self.chip_of = chip_of or (lambda pos: int(pos))
+        self._local = threading.local()
+        self._lock = threading.Lock()
+        self._free = []
+        self._gens = []
+        self.max_obs = max(dates(cfg, c).shape[0] for c in range(64))  # base cadence / sidelap
+        self.allocated = 0
+        self.generate_seconds = 0.0
+
+    def _gen(self):
+        g = getattr(self._local, 'gen', None)
+        if g is None:
+            g = self._local.gen = DeviceGenerator(self.device)
+            with self._lock:
+                self._gens.append(g)
+        return g
+
+    def __call__(self, positions):
+        import time
+        import ccdgpu
+        g = self._gen()
+        ids = [self.chip_of(p) for p in positions]
+        if len(ids) > self.batch_chips:
+            raise ValueError('%d chips in one batch, the pool holds %d' % (len(ids), self.batch_chips))
+        nobs = [g.dates(self.cfg, c).shape[0] for c in ids]
+        if max(nobs) > self.max_obs:
+            raise ValueError('chip with %d observations past the pool buffers (%d)' % (max(nobs), self.max_obs))
+        with self._lock:
+            st = self._free.pop() if self._free else None
+            if st is None:
+                self.allocated += 1
+        if st is None:
+            st = ccdgpu.batch_storage(self.batch_chips, self.n_pix, self.max_obs)
+        b = ccdgpu.ChipBatch([self.n_pix] * len(ids), nobs, storage=st)
+        t = time.perf_counter()
+        g.batch(self.cfg, ids, n_pix=self.n_pix, out=b)
+        with self._lock:
+            self.generate_seconds += time.perf_counter() - t
+        return b
+
+    def release(self, batch):
+        if batch.storage is not None:
+            with self._lock:
+                self._free.append(batch.storage)
+
+    def prefill(self, n):
+        """Allocate ``n`` pool buffers ahead (page-locking is slow: keep it out of a timed run)."""
+        import ccdgpu
+        while self.allocated < n:
+            st = ccdgpu.batch_storage(self.batch_chips, self.n_pix, self.max_obs)
+            with self._lock:
+                self._free.append(st)
+                self.allocated += 1
+
+    def close(self):
+        for g in self._gens:
+            g.close()
+        self._gens = []

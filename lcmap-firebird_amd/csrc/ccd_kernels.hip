@@ -267,6 +267,22 @@ __device__ __forceinline__ uint4 crow4(const Px &P, int j, int line) {
 #define CVR(P, b, j) cvr(P, (b), (j), __LINE__)
 
 // ------------------------------------------------------------------ wave primitives
+// Every primitive below that reads other lanes' registers (DPP, readlane, bpermute, ballot) is
+// only correct with all 64 lanes enabled: a disabled lane's register holds whatever the register
+// allocator left there.  All control flow around them is wave-uniform by construction; the
+// checking build asserts it: each primitive takes its call site's line (XL) and, when EXEC is
+// not all ones, records 100000 + line in counters[4] (CCDGPU_EHIP names it).
+#ifdef CCD_GUARD_LINES
+__device__ __forceinline__ void exec_full(int line) {
+    if (__builtin_amdgcn_read_exec() != ~0ull)
+        atomicCAS(&ARGS().counters[4], 0ull, 100000ull + (unsigned long long)line);
+}
+#define XL , int xline_ = __builtin_LINE()
+#define EXEC_FULL() exec_full(xline_)
+#else
+#define XL
+#define EXEC_FULL()
+#endif
 // Opaque like ARGS(): lane-derived masks and index maps are recomputed where they are used
 // instead of being hoisted to the kernel entry and kept live (spilled) for the whole kernel.
 __device__ __forceinline__ int lane() {
@@ -274,9 +290,25 @@ __device__ __forceinline__ int lane() {
     asm volatile("" : "+v"(l));
     return l;
 }
-__device__ __forceinline__ unsigned long long bal(bool p) { return __ballot(p); }
+__device__ __forceinline__ unsigned long long bal(bool p XL) {
+    EXEC_FULL();
+    return __ballot(p);
+}
 __device__ __forceinline__ int popc(unsigned long long x) { return __popcll(x); }
-__device__ __forceinline__ int below(unsigned long long m) {
+// lane shuffles (ds_bpermute): the source lane must be enabled
+template <class T>
+__device__ __forceinline__ T shf(T v, int src XL) {
+    EXEC_FULL();
+    return __shfl(v, src);
+}
+template <class T>
+__device__ __forceinline__ T shfx(T v, int m XL) {
+    EXEC_FULL();
+    return __shfl_xor(v, m);
+}
+
+__device__ __forceinline__ int below(unsigned long long m XL) {
+    EXEC_FULL();
     return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
 }
 // DPP lane moves on a double (two 32-bit halves).  Controls: 0xB1 quad_perm [1,0,3,2] (xor 1),
@@ -290,14 +322,16 @@ __device__ __forceinline__ double dpp(double v) {
     const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, true);
     return __hiloint2double(hi, lo);
 }
-__device__ __forceinline__ double rdlane(double v, int l) {
+__device__ __forceinline__ double rdlane(double v, int l XL) {
+    EXEC_FULL();
     return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
                             __builtin_amdgcn_readlane(__double2loint(v), l));
 }
 // Inclusive prefix sum over the 64 lanes in DPP only (no LDS round trip): Hillis-Steele with
 // row_shr 1/2/4/8 inside each row of 16, then row_bcast:15 (rows 1, 3) and row_bcast:31
 // (rows 2, 3) carry the row totals across.
-__device__ __forceinline__ int wscan_incl(int v) {
+__device__ __forceinline__ int wscan_incl(int v XL) {
+    EXEC_FULL();
     v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
     v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
     v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);
@@ -313,10 +347,14 @@ __device__ __forceinline__ int wscan_incl(int v) {
     return v;
 }
 // value of v in a (wave-uniform) lane, as a scalar
-__device__ __forceinline__ int rdl(int v, int src) { return __builtin_amdgcn_readlane(v, src); }
+__device__ __forceinline__ int rdl(int v, int src XL) {
+    EXEC_FULL();
+    return __builtin_amdgcn_readlane(v, src);
+}
 
 // wave-wide sum, identical (wave-uniform) result in every lane
-__device__ __forceinline__ double wsum(double v) {
+__device__ __forceinline__ double wsum(double v XL) {
+    EXEC_FULL();
     v += dpp<0xB1>(v);
     v += dpp<0x4E>(v);
     v += dpp<0x141>(v);
@@ -390,13 +428,14 @@ __device__ __forceinline__ double kth_nonneg(const GLOBAL_AS double *vals, int N
 }
 
 // ascending bitonic sort of one double per lane across the 64-lane wave (21 exchange stages)
-__device__ __forceinline__ double bitonic64(double v) {
+__device__ __forceinline__ double bitonic64(double v XL) {
+    EXEC_FULL();
     const int l = lane();
 #pragma unroll
     for (int k = 2; k <= W; k <<= 1) {
 #pragma unroll
         for (int j = k >> 1; j > 0; j >>= 1) {
-            const double o = __shfl_xor(v, j);
+            const double o = shfx(v, j);
             const bool up = (l & k) == 0;
             const bool lower = (l & j) == 0;
             const double mn = o < v ? o : v;
@@ -628,7 +667,8 @@ __device__ __forceinline__ void gram_finalize(const Px &P, int nw) {
 }
 
 // 8-lane group reductions (a band's lanes 8b .. 8b+7); results identical in all 8 lanes.
-__device__ __forceinline__ double gsum8(double v) {
+__device__ __forceinline__ double gsum8(double v XL) {
+    EXEC_FULL();
     v += dpp<0xB1>(v);
     v += dpp<0x4E>(v);
     return v + dpp<0x141>(v);
@@ -640,7 +680,8 @@ __device__ __forceinline__ double vmax(double a, double b) {
     asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
-__device__ __forceinline__ double gmax8(double v) {
+__device__ __forceinline__ double gmax8(double v XL) {
+    EXEC_FULL();
     v = vmax(v, dpp<0xB1>(v));
     v = vmax(v, dpp<0x4E>(v));
     return vmax(v, dpp<0x141>(v));
@@ -648,7 +689,8 @@ __device__ __forceinline__ double gmax8(double v) {
 
 // float max over a band's 8 lanes, one DPP-modified v_max_f32 per level (a 64-bit max needs two
 // lane moves and a max per level); s_nop 1: a DPP source read 2 wait states after its VALU write
-__device__ __forceinline__ float gmax8f(float v) {
+__device__ __forceinline__ float gmax8f(float v XL) {
+    EXEC_FULL();
     float r;
     asm("s_nop 1\n\t"
         "v_max_f32_dpp %0, %1, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
@@ -668,7 +710,8 @@ __device__ __forceinline__ float gmax8f(float v) {
 // Per coordinate: soft threshold (3 VALU), d (1 fused), lane J's w (1, exec-masked), 2 DPP FMAs.
 template <int J>
 __device__ __forceinline__ void cd_coord(unsigned long long mJ /* live lanes of coordinate J */,
-                                         double alpha, double rgkk, double ngcolJ, double &h, double &w) {
+                                         double alpha, double rgkk, double ngcolJ, double &h, double &w XL) {
+    EXEC_FULL();
     // sklearn: fsign(tmp) * fmax(|tmp| - alpha, 0) / norm (a signed zero below alpha, as there)
     const double s = copysign(fmax(fabs(h) - alpha, 0.0), h);
     // d = w_new - w_old in one rounding (read from lane J only; a finished group's column is
@@ -744,13 +787,15 @@ __device__ __forceinline__ int cd_sweep(Lds *L, int pc_rt, double alpha, int max
         // w_max in [2^-100, 2^100], D < fl(tol) W (1 - 2^-16) implies d/w < tol (1 - 2^-17), so
         // fl64(d/w) < tol, and D > fl(tol) W (1 + 2^-16) implies fl64(d/w) >= tol.  Groups whose
         // ratio falls in that band (or whose w_max is 0 or out of range) take the exact test.
+        // The bound needs tw = fl(tol) W and tw (1 -+ 2^-16) normal floats: with a tolerance
+        // below ~1e-8 (or flushed denormals) tw can be subnormal, so tw < 2^-125 also goes exact.
         unsigned long long rl, wz = 0ull;  // groups with d_w_max / w_max < tol, with w_max = 0
         {
             const float D = gmax8f((float)fabs(w - w0));
             const float Wf = gmax8f((float)fabs(w));  // w stays 0 in lanes outside the model
             const float tw = tol_f * Wf;
             // (one ballot per comparison: each v_cmp writes its lane mask straight to SGPRs)
-            const unsigned long long wokm = bal(Wf >= 0x1p-100f) & bal(Wf <= 0x1p100f);
+            const unsigned long long wokm = bal(Wf >= 0x1p-100f) & bal(Wf <= 0x1p100f) & bal(tw >= 0x1p-125f);
             const unsigned long long ltm = wokm & bal(D < tw * (1.0f - 0x1p-16f));
             const unsigned long long gem = wokm & bal(D > tw * (1.0f + 0x1p-16f));
             rl = ltm;
@@ -849,7 +894,7 @@ __device__ __forceinline__ void fit_models(Px &P, int a, int b, int k, bool with
     {
         int wsw = (l >> 3) < NB ? sw : 0;  // the wave's sweep count: max over the band groups
         for (int o = 32; o > 0; o >>= 1) {
-            const int t = __shfl_xor(wsw, o);
+            const int t = shfx(wsw, o);
             wsw = t > wsw ? t : wsw;
         }
         PH_COUNT(P, 28, wsw >= p.lasso_max_iter ? 1 : 0)
@@ -898,7 +943,7 @@ __device__ __forceinline__ void emit(Px &P, int sday, int eday, int bday, int co
     const int l = lane();
     unsigned long long slot = 0;
     if (l == 0) slot = atomicAdd(&A.counters[1], 1ull);
-    slot = __shfl((unsigned long long)slot, 0);
+    slot = shf((unsigned long long)slot, 0);
     if (slot >= (unsigned long long)A.pool_cap) {
         if (l == 0) atomicOr(&A.counters[3], 1ull);
         P.nseg++;
@@ -1499,8 +1544,8 @@ __device__ __forceinline__ int tmask_reg(Px &P, int a, int b) {
             // mad = median(sort(|r|)[4:]) / 0.6745: one value per lane, bitonic sort across the wave
             const int c = nw - 4;
             const double v = bitonic64(in ? fabs(rr) : __builtin_inf());
-            const double hi = __shfl(v, 4 + c / 2);
-            const double lo = __shfl(v, 4 + (c - 1) / 2);
+            const double hi = shf(v, 4 + c / 2);
+            const double lo = shf(v, 4 + (c - 1) / 2);
             const double med = (c & 1) ? hi : (lo + hi) / 2.0;
             const double mad = med / 0.6745;
             const double floor_ = 2.220446049250313e-16 * ystd;
@@ -1531,7 +1576,7 @@ __device__ __forceinline__ int tmask_reg(Px &P, int a, int b) {
     }
     int cnt = 0;
     for (int i = l; i < (nw + 31) / 32; i += W) cnt += __popc(L->tflag[i]);
-    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+    for (int o = 32; o > 0; o >>= 1) cnt += shfx(cnt, o);
     wsync();
     return cnt;
 }
@@ -1628,8 +1673,8 @@ __device__ __forceinline__ int tmask(Px &P, int a, int b) {
             if (nw <= W) {
                 // one value per lane (lane i wrote absr[i]): bitonic sort across the wave
                 const double v = bitonic64(l < nw ? absr[l] : __builtin_inf());
-                const double hi = __shfl(v, 4 + c / 2);
-                const double lo = __shfl(v, 4 + (c - 1) / 2);
+                const double hi = shf(v, 4 + c / 2);
+                const double lo = shf(v, 4 + (c - 1) / 2);
                 med = (c & 1) ? hi : (lo + hi) / 2.0;
             } else if (c & 1) {
                 med = kth_nonneg(absr, nw, 4 + c / 2);
@@ -1675,7 +1720,7 @@ __device__ __forceinline__ int tmask(Px &P, int a, int b) {
     }
     int cnt = 0;
     for (int i = l; i < (nw + 31) / 32; i += W) cnt += __popc(L->tflag[i]);
-    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+    for (int o = 32; o > 0; o >>= 1) cnt += shfx(cnt, o);
     wsync();
     return cnt;
 }
@@ -1794,7 +1839,7 @@ __device__ __forceinline__ bool eval_peek(Px &P, int k, int start, int dir, doub
         const double v = r / rm;
         const double mag = gsum8((valid && det) ? v * v : 0.0);
         if (bal(bnd == 0 && jj < k && !(mag > L->chg))) all = false;
-        if (pass == 0) mag0 = __shfl(mag, 0);
+        if (pass == 0) mag0 = shf(mag, 0);
     }
     stat_uniform(ST_FLOPS, (unsigned long long)k * (7 * 2 * 8 + 5 * 3));
     PH_COUNT(P, 18, 1)  // predict 7*2*8 + magnitude 5*3 per peek obs
@@ -2666,7 +2711,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
             // later), so the first such step under that assumption bounds the batch from below:
             // lanes more than 2 steps past it are left out (with more removals before it the batch
             // ends there without a terminal step and the next one continues).
-            const int dp = __shfl(dj, l > 0 ? l - 1 : 0);
+            const int dp = shf(dj, l > 0 ? l - 1 : 0);
             const bool t0 = valid && ((double)(l > 0 ? dp : dprev) - (double)da) >= 1.33 * fit_span;
             const unsigned long long T0 = bal(t0);
             const int lim = T0 ? __ffsll((long long)T0) + 1 : W;  // first such step + 2
@@ -2716,7 +2761,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
         const unsigned long long O = bal(valid && outj);
         const unsigned long long lower = (V & ~O) & ((1ull << l) - 1ull);
         const int lk = lower ? 63 - __clzll(lower) : 0;
-        const int dsh = __shfl(dj, lk);
+        const int dsh = shf(dj, lk);
         const int dlk = lower ? dsh : dprev;  // date at position b - 1 when step l starts
         const bool trig = valid && ((double)dlk - (double)da) >= 1.33 * fit_span;
         const unsigned long long TG = bal(trig);
@@ -2916,10 +2961,10 @@ __device__ __forceinline__ int px_setup(Px &P, int chip, int pix) {
         const unsigned long long km = bal(keep);
         const unsigned long long lower = l ? (km & ((1ull << l) - 1ull)) : 0ull;
         const int pl = lower ? 63 - __clzll(lower) : l;
-        const int pd = __shfl(d, pl);
+        const int pd = shf(d, pl);
         const int prevd = lower ? pd : carry;
         const bool keep2 = keep && d != prevd;
-        if (km) carry = __shfl(d, 63 - __clzll(km));
+        if (km) carry = shf(d, 63 - __clzll(km));
         const unsigned long long k2 = bal(keep2);
         if (keep2) {
             const int pos = gidx(P, m + below(k2), n, __LINE__);
@@ -2974,7 +3019,7 @@ __device__ __forceinline__ void detect_body() {
     for (;;) {
         unsigned long long job = 0;
         if (l == 0) job = atomicAdd(&A.counters[0], 1ull);
-        job = __shfl((unsigned long long)job, 0);
+        job = shf((unsigned long long)job, 0);
         if (job >= (unsigned long long)A.total_pix) break;
         // chip of this pixel: binary search of the chips' pixel offsets (wave-uniform)
         int lo = 0, hi = A.n_chips - 1;
@@ -3043,7 +3088,7 @@ __device__ __forceinline__ void detect_body() {
     {
         int bl = P.bad;
         for (int o = 32; o > 0; o >>= 1) {
-            const int t = __shfl_xor(bl, o);
+            const int t = shfx(bl, o);
             bl = t > bl ? t : bl;
         }
         if (l == 0 && bl) atomicCAS(&A.counters[4], 0ull, (unsigned long long)bl);

@@ -639,6 +639,9 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         unsigned long long h[8];
         HIPCHK(hipMemcpyAsync(h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
+        if (h[4] >= 100000)
+            return fail(CCDGPU_EHIP, "cross-lane primitive ran without a full EXEC at ccd_kernels.hip line " +
+                                         std::to_string(h[4] - 100000));
         if (h[4]) return fail(CCDGPU_EHIP, "kernel index guard tripped at ccd_kernels.hip line " + std::to_string(h[4]));
         if (h[3]) {  // pool overflow: grow and rerun
             c->pool_cap = (int64_t)(h[1] + h[1] / 4 + 1024);

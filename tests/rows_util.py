@@ -49,10 +49,11 @@ class OracleContext(object):
     """Stand-in for ccdgpu.Context in CPU tests of the tile runner: the C oracle detects, the
     rows are restated on the host.  Same slot / fetch protocol as the device context."""
 
-    def __init__(self, device=0, threads=2, delay=0.0):
+    def __init__(self, device=0, threads=2, delay=0.0, fail=None):
         self.device = device
         self.threads = threads
         self.delay = delay
+        self.fail = fail  # an exception raised by run_slot (error-path tests of the runner)
         self.qa_error = False
         self._slots = {}
         self._results = None
@@ -64,6 +65,8 @@ class OracleContext(object):
         import time
         import oracle_ctypes
         batch, params = self._slots.pop(slot)
+        if self.fail is not None:
+            raise self.fail
         out = []
         for c in range(batch.n_chips):
             d, s, q = batch.chip(c)

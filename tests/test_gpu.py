@@ -55,6 +55,9 @@ def test_chip_vs_oracle(ctx, which, chip, n_pix):
     {'DETECTION_BANDS': [0, 1, 2, 3, 4, 5, 6]},
     {'KELVIN_TO_CELSIUS': False, 'THERMAL_MIN': 1800, 'THERMAL_MAX': 3400},
     {'COEFFICIENT_MAX': 6, 'LASSO_MAX_ITER': 50},
+    # tolerances whose float32 pre-check product would be subnormal: the exact test decides
+    {'LASSO_TOL': 1e-10, 'LASSO_MAX_ITER': 200},
+    {'LASSO_TOL': 1e-40, 'LASSO_MAX_ITER': 60},
 ])
 def test_param_variants_vs_oracle(ctx, params):
     d, s, q = synth.chip(synth.config(5), 4, 0, 300)

@@ -107,3 +107,60 @@ def test_tile_run_world2_shares_one_queue_and_gathers_on_rank0():
                                  context_factory=lambda dev: OracleContext(dev, threads=2))
     assert [c['digest'] for c in res['chips']] == [c['digest'] for c in ref['chips']]
     assert res['xys'] == ref['xys']
+
+
+def _failing_rank(rank, world, port, q):
+    sys.path[:0] = [os.path.join(ROOT, 'tests'), os.path.join(ROOT, 'oracle'), os.path.join(ROOT, 'lcmap-firebird_amd')]
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group('gloo', rank=rank, world_size=world, timeout=__import__('datetime').timedelta(seconds=120))
+    from ccdc import runner
+    from rows_util import OracleContext
+    fail = RuntimeError('injected device failure') if rank == 1 else None
+    try:
+        runner.changedetection(tile(), source, contexts=1, batch_chips=1, number=N_CHIPS,
+                               context_factory=lambda dev: OracleContext(dev, threads=2, fail=fail))
+        q.put((rank, 'no error'))
+    except runner.TileError as e:
+        q.put((rank, ('TileError', e.rank, str(e))))
+    except Exception as e:
+        q.put((rank, (type(e).__name__, str(e))))
+    dist.destroy_process_group()
+
+
+def test_tile_run_world2_reports_a_failed_rank_without_hanging():
+    """A worker failure on rank 1 reaches rank 0 as a TileError naming rank 1 and the cause;
+    rank 1 raises its own error; neither rank waits for the process-group timeout."""
+    import time
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    t = time.time()
+    procs = [ctx.Process(target=_failing_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert out[0][0] == 'TileError' and out[0][1] == 1 and 'injected device failure' in out[0][2], out
+    assert out[1] == ('RuntimeError', 'injected device failure'), out
+    assert time.time() - t < 100
+
+
+def test_runner_rejects_an_upload_depth_past_the_slots():
+    from ccdc import runner
+    from rows_util import OracleContext
+    with pytest.raises(ValueError, match='upload_depth'):
+        runner.changedetection(tile(), source, contexts=1, batch_chips=1, number=2, upload_depth=4,
+                               context_factory=lambda dev: OracleContext(dev, threads=1))
+
+
+def test_tail_batches_shrink_near_the_end_of_the_queue():
+    from ccdc import runner
+    q = runner.LocalQueue(40)
+    assert runner._pull_size(q, 8, 16) == 8
+    q.next(30)
+    assert runner._pull_size(q, 8, 16) == 2
