@@ -69,6 +69,8 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-packer', action='store_true', help='skip the chip-packer (chipmunk decode) leg')
     ap.add_argument('--tile-chips', type=int, default=TILE_CHIPS, help='chips of the headline tile leg per rank')
+    ap.add_argument('--no-tile', action='store_true',
+                    help='resident leg only (kernel A/B runs): value = the resident rate, not the headline metric')
     ap.add_argument('--tile-batch', type=int, default=8, help='chips per launch in the tile leg')
     ap.add_argument('--tile-contexts', type=int, default=2, help='contexts per GPU in the tile leg')
     ap.add_argument('--tile-depth', type=int, default=2, help='batches each tile-leg context keeps uploaded ahead')
@@ -163,6 +165,19 @@ def main():
     n_devices = min(world, ndev) if args.share_device else world
 
     res = resident_leg(args, cfg, rank, world, device, dist)
+    if args.no_tile:
+        if rank == 0:
+            res.pop('batch')
+            out = {'metric': 'resident detection rate (kernel A/B run, not the headline metric)', 'value': res['value'],
+                   'unit': 'pixels/s', 'n_gpus': n_devices, 'steps': args.steps, 'warmup': args.warmup,
+                   'ms_per_step': res['ms_per_step'], 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+                   'dtype': 'f64', 'data': 'synthetic', 'config': {'workload': res['workload'],
+                                                                  'workload_key': res['workload_key']},
+                   'roofline': res['roofline'], 'resident': res}
+            print(json.dumps(out), file=json_out, flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
     tl = tile_leg(args, cfg, rank, world, device, dist)
     if rank == 0:
         out = {
@@ -218,14 +233,15 @@ def main():
         dist.destroy_process_group()
 
 
-def resident_leg(args, cfg, rank, world, device, dist):
+def resident_leg(args, cfg, rank, world, device, dist, batch=None):
     """The detection hot path alone, inputs resident in HBM: the rank's ``--chips`` tile chips
     (the tile's cadence mix, spread over the tile) staged once as ONE ragged batch; K steps of
     prep + detect + scan + scatter, two contexts alternating so a launch overlaps the previous
     one's tail.  Behind the roofline."""
     import ccdgpu
     ids = chip_ids(rank, args.chips, world, lambda c: synth_nobs(cfg, c))
-    batch = build_batch(cfg, ids)
+    if batch is None:
+        batch = build_batch(cfg, ids)
     ctxs = [ccdgpu.Context(device) for _ in range(max(1, args.contexts))]
     for c in ctxs:
         c.stage_chips(batch)
@@ -366,7 +382,8 @@ def tile_leg(args, cfg, rank, world, device, dist):
     warm_total = world * min(per_rank, args.warmup * chips_per_step)
     src_timed = synth.TileSource(cfg, device=device, batch_chips=B, chip_of=lambda p: p)
     src_warm = synth.TileSource(cfg, device=device, batch_chips=B, chip_of=lambda p: 1000000 + p)
-    pool = args.tile_contexts * (args.tile_depth + 1) + args.tile_contexts
+    # pinned batches in flight per context: depth + 1 staged, one fetched and waiting, one being fetched
+    pool = args.tile_contexts * (args.tile_depth + 3)
     src_timed.prefill(pool)
     src_warm._free = src_timed._free  # one pinned pool for both phases
     src_warm.allocated = src_timed.allocated

@@ -142,11 +142,43 @@ def _pull_size(queue, batch_chips, tail_chips):
     return batch_chips
 
 
+def _fetcher(queue, source, batch_chips, tail_chips, stats, ready, stop):
+    """A worker's fetch thread: pulls the next positions from the shared queue and asks the source
+    for their ARD (the merlin / chipmunk fetch stand-in; often I/O- or copy-bound), so the fetch
+    of the next batches overlaps the upload, detection and row fetch of the current ones.  Puts
+    (positions, batch) on ``ready`` (bounded: one batch waits while the next is fetched), then
+    None when the queue is empty, or the exception that stopped it."""
+    clock = time.perf_counter
+    try:
+        while not stop.is_set():
+            t0 = clock()
+            pos = queue.next(_pull_size(queue, batch_chips, tail_chips))
+            if not pos:
+                with stats['lock']:
+                    stats['queue_empty_at'] = max(stats['queue_empty_at'], t0 - stats['t0'])
+                ready.put(None)
+                return
+            batch = source(pos)
+            if batch.n_chips != len(pos):
+                raise ValueError('source returned %d chips for %d positions' % (batch.n_chips, len(pos)))
+            with stats['lock']:
+                stats['source_seconds'] += clock() - t0
+            ready.put((pos, batch))
+    except BaseException as e:
+        ready.put(e)
+
+
 def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, errors, depth=2, tail_chips=0):
     """One context: up to ``depth`` batches uploaded (or uploading) ahead of the one being
     detected, one upload slot each, so the PCIe link stays busy while a batch is detected and
     its rows are fetched (with one batch ahead the link idles whenever both of a GPU's contexts
-    are past their upload).  Near the end of the queue the batches shrink (``_pull_size``)."""
+    are past their upload).  The ARD of the next batches is fetched by the worker's own fetch
+    thread (``_fetcher``) meanwhile.  Near the end of the queue the batches shrink (``_pull_size``)."""
+    import queue as queue_mod
+    ready = queue_mod.Queue(maxsize=1)  # one fetched batch waiting (+ one being fetched)
+    stop = threading.Event()
+    ft = threading.Thread(target=_fetcher, args=(queue, source, batch_chips, tail_chips, stats, ready, stop), daemon=True)
+    ft.start()
     try:
         clock = time.perf_counter
         free = list(range(depth + 1))
@@ -154,24 +186,23 @@ def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, er
         exhausted = False
         while True:
             while free and not exhausted:
-                t0 = clock()
-                pos = queue.next(_pull_size(queue, batch_chips, tail_chips))
-                if not pos:
-                    exhausted = True
-                    with stats['lock']:
-                        stats['queue_empty_at'] = max(stats['queue_empty_at'], t0 - stats['t0'])
+                # with a batch staged, upload only what is already fetched; otherwise wait for it
+                try:
+                    item = ready.get(block=not staged)
+                except queue_mod.Empty:
                     break
-                batch = source(pos)
-                if batch.n_chips != len(pos):
-                    raise ValueError('source returned %d chips for %d positions' % (batch.n_chips, len(pos)))
+                if item is None:
+                    exhausted = True
+                    break
+                if isinstance(item, BaseException):
+                    raise item
+                pos, batch = item
                 t1 = clock()
                 slot = free.pop(0)
                 ctx.stage_slot_chips(slot, batch, params)
                 staged.append((slot, pos, batch))
-                t2 = clock()
                 with stats['lock']:
-                    stats['source_seconds'] += t1 - t0
-                    stats['stage_seconds'] += t2 - t1
+                    stats['stage_seconds'] += clock() - t1
             if not staged:
                 break
             s, ppos, pbatch = staged.pop(0)
@@ -205,6 +236,14 @@ def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, er
                 stats['sink_seconds'] += t5 - t4
     except BaseException as e:  # reported by detect_tile after the other workers drain
         errors.append(e)
+    finally:
+        stop.set()
+        while ft.is_alive():  # unblock a fetcher waiting to put (its batch is dropped)
+            try:
+                ready.get(timeout=0.05)
+            except queue_mod.Empty:
+                pass
+        ft.join()
 
 
 def detect_tile(xys, source, queue, device=0, contexts=2, batch_chips=16, params=None, width=100,

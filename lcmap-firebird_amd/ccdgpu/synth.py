@@ -39,7 +39,7 @@ def lib():
         L.ccdsynth_gpu_create.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
         L.ccdsynth_gpu_destroy.argtypes = [ctypes.c_void_p]
         L.ccdsynth_gpu_error.restype = ctypes.c_char_p
-        L.ccdsynth_gpu_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(SynthCfg), ctypes.c_int32] + [ctypes.c_void_p] * 10
+        L.ccdsynth_gpu_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(SynthCfg), ctypes.c_int32] + [ctypes.c_void_p] * 9
         _lib = L
     return _lib
 
@@ -143,8 +143,9 @@ class TileSource(object):
     ``release(batch)`` once its rows are fetched; the pool grows when every buffer is in use.
     ``generate_seconds`` sums the time spent generating (GPU kernel + device-to-host copy)."""
 
-    def __init__(self, cfg, device=0, batch_chips=8, n_pix=10000, chip_of=None):
+    def __init__(self, cfg, device=0, batch_chips=8, n_pix=10000, chip_of=None, pinned=True):
         import threading
+        self.pinned = pinned
         self.cfg = cfg
         self.device = int(device)
         self.batch_chips = int(batch_chips)
@@ -181,7 +182,7 @@ class TileSource(object):
             if st is None:
                 self.allocated += 1
         if st is None:
-            st = ccdgpu.batch_storage(self.batch_chips, self.n_pix, self.max_obs)
+            st = ccdgpu.batch_storage(self.batch_chips, self.n_pix, self.max_obs, pinned=self.pinned)
         b = ccdgpu.ChipBatch([self.n_pix] * len(ids), nobs, storage=st)
         t = time.perf_counter()
         g.batch(self.cfg, ids, n_pix=self.n_pix, out=b)
@@ -198,7 +199,7 @@ class TileSource(object):
         """Allocate ``n`` pool buffers ahead (page-locking is slow: keep it out of a timed run)."""
         import ccdgpu
         while self.allocated < n:
-            st = ccdgpu.batch_storage(self.batch_chips, self.n_pix, self.max_obs)
+            st = ccdgpu.batch_storage(self.batch_chips, self.n_pix, self.max_obs, pinned=self.pinned)
             with self._lock:
                 self._free.append(st)
                 self.allocated += 1

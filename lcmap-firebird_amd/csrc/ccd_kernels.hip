@@ -81,6 +81,7 @@ struct __attribute__((aligned(16))) Lds {
         struct {
             uint32_t tflag[MAXW];  // Tmask outlier flags of the current window
             double tchol[5][5];    // Tmask: Cholesky factor of the unweighted normal matrix
+            double tsys[2][5][6];  // paired Tmask: each band's weighted normal matrix | rhs
         };
     };
     // launch statistics of this wave (kept here, not in registers: they are only touched per fit
@@ -267,15 +268,20 @@ __device__ __forceinline__ uint4 crow4(const Px &P, int j, int line) {
 #define CVR(P, b, j) cvr(P, (b), (j), __LINE__)
 
 // ------------------------------------------------------------------ wave primitives
-// Every primitive below that reads other lanes' registers (DPP, readlane, bpermute, ballot) is
-// only correct with all 64 lanes enabled: a disabled lane's register holds whatever the register
-// allocator left there.  All control flow around them is wave-uniform by construction; the
-// checking build asserts it: each primitive takes its call site's line (XL) and, when EXEC is
-// not all ones, records 100000 + line in counters[4] (CCDGPU_EHIP names it).
+// Every primitive below that reads other lanes' registers (DPP, readlane, bpermute) is only
+// correct with all 64 lanes enabled: a disabled lane's register holds whatever the register
+// allocator left there.  (Ballots and mbcnt are lane-local -- a v_cmp writes 0 for a disabled
+// lane -- and need no full EXEC.)  All control flow around them is wave-uniform by construction;
+// the checking build asserts it: each primitive takes its call site's line (XL) and, when EXEC
+// is not all ones, records 100000 + line in counters[4] (the first; CCDGPU_EHIP names it) and
+// sets bit line / 2 of the bitmap in stats[8 ..] (all of them; the host lists them).
 #ifdef CCD_GUARD_LINES
 __device__ __forceinline__ void exec_full(int line) {
-    if (__builtin_amdgcn_read_exec() != ~0ull)
+    if (__builtin_amdgcn_read_exec() != ~0ull) {
         atomicCAS(&ARGS().counters[4], 0ull, 100000ull + (unsigned long long)line);
+        const int bit = line >> 1;
+        if (bit < 64 * (CCD_NSTATS - 8)) atomicOr(&ARGS().stats[8 + (bit >> 6)], 1ull << (bit & 63));
+    }
 }
 #define XL , int xline_ = __builtin_LINE()
 #define EXEC_FULL() exec_full(xline_)
@@ -290,10 +296,7 @@ __device__ __forceinline__ int lane() {
     asm volatile("" : "+v"(l));
     return l;
 }
-__device__ __forceinline__ unsigned long long bal(bool p XL) {
-    EXEC_FULL();
-    return __ballot(p);
-}
+__device__ __forceinline__ unsigned long long bal(bool p) { return __ballot(p); }
 __device__ __forceinline__ int popc(unsigned long long x) { return __popcll(x); }
 // lane shuffles (ds_bpermute): the source lane must be enabled
 template <class T>
@@ -307,8 +310,7 @@ __device__ __forceinline__ T shfx(T v, int m XL) {
     return __shfl_xor(v, m);
 }
 
-__device__ __forceinline__ int below(unsigned long long m XL) {
-    EXEC_FULL();
+__device__ __forceinline__ int below(unsigned long long m) {
     return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
 }
 // DPP lane moves on a double (two 32-bit halves).  Controls: 0xB1 quad_perm [1,0,3,2] (xor 1),
@@ -437,6 +439,27 @@ __device__ __forceinline__ double bitonic64(double v XL) {
         for (int j = k >> 1; j > 0; j >>= 1) {
             const double o = shfx(v, j);
             const bool up = (l & k) == 0;
+            const bool lower = (l & j) == 0;
+            const double mn = o < v ? o : v;
+            const double mx = o < v ? v : o;
+            v = (lower == up) ? mn : mx;
+        }
+    }
+    return v;
+}
+
+// two independent ascending bitonic sorts, lanes 0..31 and 32..63 (the 64-lane network without
+// its last merge, the k = 32 stage ascending in both halves): the same sorted sequence per half as
+// bitonic64 gives for 32 values padded with +inf
+__device__ __forceinline__ double bitonic32x2(double v XL) {
+    EXEC_FULL();
+    const int l = lane();
+#pragma unroll
+    for (int k = 2; k <= 32; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const double o = shfx(v, j);
+            const bool up = k == 32 || (l & k) == 0;
             const bool lower = (l & j) == 0;
             const double mn = o < v ? o : v;
             const double mx = o < v ? v : o;
@@ -1581,12 +1604,239 @@ __device__ __forceinline__ int tmask_reg(Px &P, int a, int b) {
     return cnt;
 }
 
+// ---- Tmask of the two default Tmask bands at once, for windows of at most 32 observations (the
+// initialize windows, nearly always): band A (the lower band) in lanes 0..31, band B in lanes
+// 32..63, lane = window observation within the half.  Every per-band quantity is computed with
+// the arithmetic of tmask_reg, in the same order: the half-wave sums equal wsum's value when the
+// other half is zero, the two 32-lane sorts give bitonic64's first 32 values, the weighted normal
+// equations of both bands accumulate in one pass over the staged rows (row = x0..x4, wA, yA, wB,
+// yB; lane = (band, matrix entry)), and each half solves its band's system.  A band whose IRLS
+// has converged (or reached its 5th fit) keeps its coefficients while the other one iterates.
+// Half-wave sum (wsum's butterfly, then the two row totals of the lane's half).
+__device__ __forceinline__ double hsum2(double v XL) {
+    EXEC_FULL();
+    v += dpp<0xB1>(v);
+    v += dpp<0x4E>(v);
+    v += dpp<0x141>(v);
+    v += dpp<0x140>(v);
+    const double s0 = rdlane(v, 0) + rdlane(v, 16);
+    const double s1 = rdlane(v, 32) + rdlane(v, 48);
+    return lane() >= 32 ? s1 : s0;
+}
+
+// acc += w x_ea x_eb over staged rows 0 .. cnt4 - 1 with the weight in column wc (tm_rows_acc's
+// arithmetic and order)
+__device__ __forceinline__ void tm_rows_acc_w(const Lds *L, int cnt4, int wc, int ea, int eb, double &acc) {
+    for (int r = 0; r < cnt4; r += 4) {
+        double wv[4], xa[4], xb[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            wv[u] = L->row[r + u][wc];
+            xa[u] = L->row[r + u][ea];
+            xb[u] = L->row[r + u][eb];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += wv[u] * xa[u] * xb[u];
+    }
+}
+
+// both bands' normal systems [G | rhs] into L->tsys[half]: rows staged by the observation lanes
+// (x, each half its weight and value), entries accumulated by lanes (half, e), e < 20 (e < 15: the
+// upper triangle of G, 15..19: rhs); with_g = false sums the rhs only
+__device__ __forceinline__ void tm_normal_pair(const double (&x)[5], double wv, double yv, int nw, int ncol, bool with_g) {
+    Lds *L = &LDS();
+    const int l = lane();
+    const int hf = l >> 5, i = l & 31;
+    const int cnt4 = (nw + 3) & ~3;  // rows nw .. cnt4 - 1 staged as zeros (add nothing)
+    if (i < cnt4) {
+        const bool rv = i < nw;
+        double *row = L->row[i];
+        if (hf == 0) {
+#pragma unroll
+            for (int r = 0; r < 5; ++r) row[r] = rv ? x[r] : 0.0;
+        }
+        row[5 + 2 * hf] = rv ? wv : 0.0;
+        row[6 + 2 * hf] = rv ? yv : 0.0;
+    }
+    wsync();
+    int ea = -1, eb = -1;
+    if (i < 15) {
+        int e = i, r = 0;
+        while (e > r) { e -= r + 1; ++r; }
+        ea = r;
+        eb = e;
+    } else if (i < 20) {
+        ea = i - 15;
+        eb = 6 + 2 * hf;
+    }
+    double acc = 0.0;
+    if (ea >= 0 && (with_g || i >= 15)) tm_rows_acc_w(L, cnt4, 5 + 2 * hf, ea, eb, acc);
+    wsync();
+    if (i < 15) {
+        if (with_g) {
+            L->tsys[hf][ea][eb] = acc;
+            L->tsys[hf][eb][ea] = acc;
+        }
+    } else if (i < 20) {
+        L->tsys[hf][ea][5] = acc;
+    }
+    wsync();
+    if (with_g && ncol == 3 && i == 0) {
+        L->tsys[hf][3][3] = 1.0;
+        L->tsys[hf][4][4] = 1.0;
+    }
+    wsync();
+}
+
+__device__ __forceinline__ int tmask_pair(Px &P, int a, int b, int bandA, int bandB) {
+    const ccdgpu_params &p = ARGS().p;
+    Lds *L = &LDS();
+    const int l = lane();
+    const int hf = l >> 5, i = l & 31;
+    const int band = hf ? bandB : bandA;
+    const int nw = b - a;
+    const double w = 2.0 * M_PI / p.avg_days_yr;
+    const double oc = w / ceil(((double)CDR(P, b - 1) - (double)CDR(P, a)) / p.avg_days_yr);
+    const int ncol = (oc == w) ? 3 : 5;
+    const bool in = i < nw;
+    double x[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    uint4 q = {0u, 0u, 0u, 0u};  // the observation's row: band values + sorted index
+    if (in) {
+        q = CROW4(P, a + i);
+        const GLOBAL_AS double *bs = P.basis + (size_t)gidx(P, (int)(q.w >> 16), P.n, __LINE__) * CCD_BASIS_STRIDE;
+        x[0] = bs[1];
+        x[1] = bs[2];
+        if (ncol == 5) {
+            double sv, cv;
+            sincos(oc * (double)CDR(P, a + i), &sv, &cv);
+            x[2] = cv;
+            x[3] = sv;
+            x[4] = 1.0;
+        } else {
+            x[2] = 1.0;
+        }
+    }
+    if (l == 0) L->tflag[0] = 0u;
+    // unweighted normal matrix (tmask_reg's: rows from lanes 0 .. nw-1, which are half A's)
+    bool ok0;
+    {
+        double G0[5][5], rhs0[5];
+        tm_normal_reg(x, 1.0, 0.0, nw, ncol);
+        tm_load(L, G0, rhs0);
+        ok0 = chol5(G0);
+        if (l == 0)
+#pragma unroll
+            for (int r = 0; r < 5; ++r)
+#pragma unroll
+                for (int c = 0; c < 5; ++c) L->tchol[r][c] = G0[r][c];
+    }
+    wsync();
+    double adj = 0.0;
+    if (in) {
+        double h = 0.9999;
+        if (ok0) {
+            double z[5], hh = 0.0;
+#pragma unroll
+            for (int r = 0; r < 5; ++r) {
+                double s2 = x[r];
+#pragma unroll
+                for (int k = 0; k < r; ++k) s2 -= L->tchol[r][k] * z[k];
+                z[r] = s2 / L->tchol[r][r];
+                hh += z[r] * z[r];
+            }
+            h = hh < 0.9999 ? hh : 0.9999;
+        }
+        adj = 1.0 / sqrt(1.0 - h);
+    }
+    const unsigned word = (band >> 1) == 0 ? q.x : (band >> 1) == 1 ? q.y : (band >> 1) == 2 ? q.z : q.w;
+    const double yv = in ? (double)(int16_t)(word >> ((band & 1) * 16)) : 0.0;
+    // y statistics (np.std, population)
+    const double ym = hsum2(yv) / nw;
+    const double dy = in ? yv - ym : 0.0;
+    const double ystd = sqrt(hsum2(dy * dy) / nw);
+    // OLS: the unweighted matrix's factor and each band's rhs
+    double coef[5], coef0[5];
+    tm_normal_pair(x, 1.0, yv, nw, ncol, false);
+    {
+        double rhs[5];
+#pragma unroll
+        for (int r = 0; r < 5; ++r) rhs[r] = L->tsys[hf][r][5];
+        if (ok0) {
+            double Gt[5][5];
+#pragma unroll
+            for (int r = 0; r < 5; ++r)
+#pragma unroll
+                for (int c = 0; c < 5; ++c) Gt[r][c] = L->tchol[r][c];
+            chol5_solve(Gt, rhs, coef);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 5; ++r) coef[r] = 0.0;  // tm_solve of the unweighted matrix: not SPD
+        }
+    }
+    int iteration = 1;
+    bool converged = false;
+    while (bal(!converged && iteration < 5)) {
+        const bool run = !converged && iteration < 5;  // this half's band still iterates
+#pragma unroll
+        for (int r = 0; r < 5; ++r) coef0[r] = coef[r];
+        const double rr = in ? (yv - tm_dot(x, coef0)) * adj : 0.0;  // signed, adjusted residual
+        // mad = median(sort(|r|)[4:]) / 0.6745: each half sorts its band's 32 values
+        const int c = nw - 4;
+        const double v = bitonic32x2(in ? fabs(rr) : __builtin_inf());
+        const double hi = shf(v, (l & 32) + 4 + c / 2);
+        const double lo = shf(v, (l & 32) + 4 + (c - 1) / 2);
+        const double med = (c & 1) ? hi : (lo + hi) / 2.0;
+        const double mad = med / 0.6745;
+        const double floor_ = 2.220446049250313e-16 * ystd;
+        const double scale = mad > floor_ ? mad : floor_;
+        const double u = rr / scale;
+        const double qq = u / 4.685;
+        const double om = 1.0 - qq * qq;
+        const double wt = fabs(u) < 4.685 ? om * om : 0.0;
+        tm_normal_pair(x, in ? wt : 0.0, yv, nw, ncol, true);
+        double Gw[5][5], rw[5], cn[5];
+#pragma unroll
+        for (int r = 0; r < 5; ++r) {
+            rw[r] = L->tsys[hf][r][5];
+#pragma unroll
+            for (int cc = 0; cc < 5; ++cc) Gw[r][cc] = L->tsys[hf][r][cc];
+        }
+        tm_solve(Gw, rw, cn);
+        bool conv = true;
+#pragma unroll
+        for (int r = 0; r < 5; ++r) {
+            coef[r] = run ? cn[r] : coef0[r];
+            if (coef[r] - coef0[r] > 1e-8) conv = false;
+        }
+        converged = run ? conv : converged;
+        iteration += run ? 1 : 0;
+    }
+    // counted flops: per band an OLS fit and each IRLS refit, n_w 35 + 5^3 each
+    {
+        const int fits = rdl(iteration, 0) + rdl(iteration, 32);  // (1 + refits) per band
+        stat_uniform(ST_FLOPS, (unsigned long long)fits * ((unsigned long long)nw * 35 + 125));
+    }
+    const double thr = L->vario[band] * p.t_const;
+    const double pr = tm_dot(x, coef) + 0.0;
+    const unsigned long long bm = bal(in && fabs(pr - yv) > thr);
+    const unsigned fl = (unsigned)bm | (unsigned)(bm >> 32);
+    if (l == 0) L->tflag[0] = fl;
+    wsync();
+    return __popc(fl);
+}
+
 // Returns the outlier count; outlier flags in L->tflag (bit i = window observation i).
 __device__ __forceinline__ int tmask(Px &P, int a, int b) {
     const ccdgpu_params &p = ARGS().p;
     Lds *L = &LDS();
     const int l = lane();
     const int nw = b - a;
+#ifndef CCD_NO_TMASK_PAIR
+    if (nw <= 32 && __builtin_popcount(p.tmask_bands & 0x7Fu) == 2) {
+        const int bA = __builtin_ctz(p.tmask_bands), bB = 31 - __builtin_clz(p.tmask_bands & 0x7Fu);
+        return tmask_pair(P, a, b, bA, bB);
+    }
+#endif
     if (nw <= W) return tmask_reg(P, a, b);
     const double w = 2.0 * M_PI / p.avg_days_yr;
     const double oc = w / ceil(((double)CDR(P, b - 1) - (double)CDR(P, a)) / p.avg_days_yr);

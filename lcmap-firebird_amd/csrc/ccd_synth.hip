@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -157,11 +158,26 @@ extern "C" int ccdsynth_gpu_batch(ccdsynth_gpu *g, const ccdsynth_cfg *cfg, int3
     delete[] jobs;
     HCK(e);
     const dim3 grid((unsigned)((max_pix + WAVES - 1) / WAVES), (unsigned)n_chips);
-    hipLaunchKernelGGL(synth_chips, grid, dim3(64 * WAVES), 0, g->stream, *cfg, (const ChipJob *)g->d_jobs,
-                       (const int64_t *)g->d_dates, (int16_t *)g->d_spectra, (uint16_t *)g->d_qa);
-    HCK(hipGetLastError());
-    HCK(hipMemcpyAsync(spectra, g->d_spectra, sizeof(int16_t) * 7 * n_data, hipMemcpyDeviceToHost, g->stream));
-    HCK(hipMemcpyAsync(qa, g->d_qa, sizeof(uint16_t) * n_data, hipMemcpyDeviceToHost, g->stream));
+    // Page-locked host buffers are written by the kernel itself, straight over PCIe (no DMA copy:
+    // the copy engines stay free for the detection path's uploads); pageable ones through HBM and a
+    // device-to-host copy.  CCDSYNTH_D2H=copy forces the latter (A/B measurements).
+    hipPointerAttribute_t as{}, aq{};
+    const char *mode = getenv("CCDSYNTH_D2H");
+    const bool direct = !(mode && !strcmp(mode, "copy")) && hipPointerGetAttributes(&as, spectra) == hipSuccess &&
+                        hipPointerGetAttributes(&aq, qa) == hipSuccess && as.type == hipMemoryTypeHost &&
+                        aq.type == hipMemoryTypeHost && as.devicePointer && aq.devicePointer;
+    (void)hipGetLastError();  // (a pageable pointer leaves an error from the attribute query)
+    if (direct) {
+        hipLaunchKernelGGL(synth_chips, grid, dim3(64 * WAVES), 0, g->stream, *cfg, (const ChipJob *)g->d_jobs,
+                           (const int64_t *)g->d_dates, (int16_t *)as.devicePointer, (uint16_t *)aq.devicePointer);
+        HCK(hipGetLastError());
+    } else {
+        hipLaunchKernelGGL(synth_chips, grid, dim3(64 * WAVES), 0, g->stream, *cfg, (const ChipJob *)g->d_jobs,
+                           (const int64_t *)g->d_dates, (int16_t *)g->d_spectra, (uint16_t *)g->d_qa);
+        HCK(hipGetLastError());
+        HCK(hipMemcpyAsync(spectra, g->d_spectra, sizeof(int16_t) * 7 * n_data, hipMemcpyDeviceToHost, g->stream));
+        HCK(hipMemcpyAsync(qa, g->d_qa, sizeof(uint16_t) * n_data, hipMemcpyDeviceToHost, g->stream));
+    }
     HCK(hipStreamSynchronize(g->stream));
     return 0;
 }

@@ -639,9 +639,21 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         unsigned long long h[8];
         HIPCHK(hipMemcpyAsync(h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
-        if (h[4] >= 100000)
+        if (h[4] >= 100000) {
+            // checking build: every call site that ran without a full EXEC, from the line bitmap
+            // (bit = line / 2) in stats[8 ..]
+            unsigned long long st[CCD_NSTATS];
+            HIPCHK(hipMemcpy(st, c->stats.p, sizeof(st), hipMemcpyDeviceToHost));
+            std::string lines;
+            for (int w = 8; w < CCD_NSTATS; ++w)
+                for (int b = 0; b < 64; ++b)
+                    if ((st[w] >> b) & 1ull) {
+                        const int l0 = 2 * (64 * (w - 8) + b);
+                        lines += (lines.empty() ? "" : ", ") + std::to_string(l0) + "-" + std::to_string(l0 + 1);
+                    }
             return fail(CCDGPU_EHIP, "cross-lane primitive ran without a full EXEC at ccd_kernels.hip line " +
-                                         std::to_string(h[4] - 100000));
+                                         std::to_string(h[4] - 100000) + " (all call sites: lines " + lines + ")");
+        }
         if (h[4]) return fail(CCDGPU_EHIP, "kernel index guard tripped at ccd_kernels.hip line " + std::to_string(h[4]));
         if (h[3]) {  // pool overflow: grow and rerun
             c->pool_cap = (int64_t)(h[1] + h[1] / 4 + 1024);

@@ -20,7 +20,7 @@ cyclic coordinate descent with the duality-gap stop) applied to the centred desi
 
 PARITY STATUS: the restatement is pinned by the reference's own boundary tests
 (``test/test_pyccd.py:33-35,37-126,129-132``: default rows, format golden, the all-fill
-4-observation detect) and by ``tests/test_oracle_sklearn.py`` (the Lasso sub-kernel against the
+4-observation detect) and by ``tests/test_oracle.py:37-61`` (the Lasso sub-kernel against the
 installed scikit-learn).  The multi-segment numeric behaviour is **parity unpinned** against
 pyccd itself: no fixture in the reference holds a pyccd change-model result.
 Every spec choice that could not be verified against the pinned pyccd source is a named

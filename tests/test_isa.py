@@ -19,7 +19,7 @@ import dpp_hazards  # noqa: E402
 import endcf_check  # noqa: E402
 
 # the w4 reproducer's shape: an `if (l < NB)` lowered without an EXEC save whose join block
-# received a spill reload (profiles/r03_w4_root_cause.md)
+# received a spill reload (profiles/r03/w4_root_cause.md)
 NARROWED_JOIN = '''_Zkernel:
 	v_cmp_gt_i32_e32 vcc, 7, v16
 	s_and_b64 s[16:17], exec, vcc

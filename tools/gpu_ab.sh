@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 T=${TAG:-ab}
 [ -n "$SKIP_TESTS" ] || timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${T}_pytest.log 2>&1 || { echo "pytest rc=$?"; tail -30 gpurun_out/${T}_pytest.log; exit 1; }
 tail -2 gpurun_out/${T}_pytest.log
-Q="--steps ${STEPS:-4} --no-cpu-baseline --no-tile --no-stream --no-packer"
+Q="--steps ${STEPS:-4} --no-cpu-baseline --no-tile --no-packer"
 for cfg in 3 ${C5:+5}; do
   for n in ${LIBS:-libccdgpu}; do
     CCDGPU_LIBRARY=$PWD/lcmap-firebird_amd/lib/$n.so timeout -k 10 300 python -u bench.py $Q --config $cfg > gpurun_out/${T}_c${cfg}_$n.json 2> gpurun_out/${T}_c${cfg}_$n.err || { echo "bench rc=$? $n"; tail -20 gpurun_out/${T}_c${cfg}_$n.err; exit 1; }

@@ -2,7 +2,7 @@
 # Developer tool: instruction/scalar cache PMC pass over one bench step.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; OUT="$R/gpurun_out"; mkdir -p "$OUT"; TAG=${1:-pmi}
-CMD="python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-packer --no-stream --chips ${CHIPS:-4}"
+CMD="python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-packer --chips ${CHIPS:-4}"
 cd /tmp && export TMPDIR=/tmp
 i=0
 for set in "SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQC_ICACHE_REQ SQ_IFETCH SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_ICACHE_BUSY_CYCLES"; do

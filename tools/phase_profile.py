@@ -2,7 +2,7 @@
 Run on the GPU box:  python tools/phase_profile.py [config] [chips]"""
 import os, sys, json
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ.setdefault('CCDGPU_LIBRARY', os.path.join(ROOT, 'lcmap-firebird_amd', 'lib', os.environ.get('CCD_DIAG_LIB', 'libccdgpu_diag.so')))
+os.environ.setdefault('CCDGPU_LIBRARY', os.path.join(ROOT, 'lcmap-firebird_amd', 'lib', 'exp', os.environ.get('CCD_DIAG_LIB', 'libccdgpu_diag.so')))
 sys.path.insert(0, os.path.join(ROOT, 'lcmap-firebird_amd'))
 import numpy as np
 import ccdgpu
