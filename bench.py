@@ -72,6 +72,7 @@ def parse():
     ap.add_argument('--no-tile', action='store_true',
                     help='resident leg only (kernel A/B runs): value = the resident rate, not the headline metric')
     ap.add_argument('--tile-batch', type=int, default=8, help='chips per launch in the tile leg')
+    ap.add_argument('--tile-pool', type=int, default=64, help='generated chips behind the tile leg\'s rotated chips')
     ap.add_argument('--tile-contexts', type=int, default=2, help='contexts per GPU in the tile leg')
     ap.add_argument('--tile-depth', type=int, default=2, help='batches each tile-leg context keeps uploaded ahead')
     ap.add_argument('--share-device', action='store_true',
@@ -349,6 +350,19 @@ def max_over_ranks(x, dist):
     return float(t.item())
 
 
+class _Offset(object):
+    """A source whose positions are shifted by ``off`` (the warmup's chips: another tile range)."""
+
+    def __init__(self, src, off):
+        self.src, self.off = src, off
+
+    def __call__(self, positions):
+        return self.src([p + self.off for p in positions])
+
+    def release(self, batch):
+        self.src.release(batch)
+
+
 class _KeptContext(object):
     """A context created before the timed region and lent to the runner (whose close() at the
     end of a tile would otherwise free it): the timed run measures the steady-state pipeline, not
@@ -380,13 +394,17 @@ def tile_leg(args, cfg, rank, world, device, dist):
     chips_per_step = -(-per_rank // K)
     total = world * per_rank
     warm_total = world * min(per_rank, args.warmup * chips_per_step)
-    src_timed = synth.TileSource(cfg, device=device, batch_chips=B, chip_of=lambda p: p)
-    src_warm = synth.TileSource(cfg, device=device, batch_chips=B, chip_of=lambda p: 1000000 + p)
+    # distinct chips: a pool of generated chips, each position a different rotation of one of them
+    # (configs 3 / 5, whose chips share two date vectors); configs 2 / 4 subsample dates per chip,
+    # so there every chip is generated on the GPU
+    mode = 'pool' if args.config in (3, 5) else 'generate'
+    src = synth.TileSource(cfg, device=device, batch_chips=B, mode=mode, pool_chips=args.tile_pool)
+    t_prep = time.perf_counter()
+    src.prepare()
     # pinned batches in flight per context: depth + 1 staged, one fetched and waiting, one being fetched
-    pool = args.tile_contexts * (args.tile_depth + 3)
-    src_timed.prefill(pool)
-    src_warm._free = src_timed._free  # one pinned pool for both phases
-    src_warm.allocated = src_timed.allocated
+    src.prefill(args.tile_contexts * (args.tile_depth + 3))
+    prep_s = time.perf_counter() - t_prep
+    src_timed = src_warm = src
     ctxs = [ccdgpu.Context(device) for _ in range(args.tile_contexts)]
     lent = iter([])
 
@@ -406,7 +424,7 @@ def tile_leg(args, cfg, rank, world, device, dist):
                                       sink=sink, upload_depth=args.tile_depth, context_factory=factory)
 
     if warm_total:
-        run(warm_total, src_warm)
+        run(warm_total, _Offset(src_warm, 1000000))
     if dist is not None:
         dist.barrier()
     ctxs[0].synchronize()
@@ -420,8 +438,7 @@ def tile_leg(args, cfg, rank, world, device, dist):
     gen_s = src_timed.generate_seconds - gen0
     for c in ctxs:
         c.close()
-    src_timed.close()
-    src_warm.close()
+    src.close()
     if res is None:
         return None
     px = sum(c['n_pix'] for c in res['chips'])
@@ -436,12 +453,16 @@ def tile_leg(args, cfg, rank, world, device, dist):
             'rows': sum(c['rows'] for c in res['chips']),
             'chips_per_rank_done': {r: st['chips'] for r, st in ranks.items()},
             'tail_seconds_per_rank': {r: round(st.get('tail_seconds', 0.0), 3) for r, st in ranks.items()},
+            'source_mode': mode, 'source_pool_chips': args.tile_pool if mode == 'pool' else None,
+            'source_prepare_seconds': round(prep_s, 2),
             'generate_seconds_rank0': round(gen_s, 3),
             'pinned_pool_batches': src_timed.allocated,
             'worker_seconds_rank0': {k: round(v, 3) for k, v in ranks[0].items() if k.endswith('_seconds')},
-            'note': 'ccdc.runner tile driver over distinct device-generated chips: GPU generation + D2H into pinned '
-                    'host batches (not excluded), H2D upload overlapped with detection, device row packing, D2H of rows, '
-                    'gather of per-chip summaries on rank 0'}
+            'note': 'ccdc.runner tile driver over distinct chips (pool mode: %d GPU-generated chips, each tile position '
+                    'one of them with every pixel series rotated by a position-dependent number of observations, '
+                    'produced by host copies into pinned batches in the runner\'s fetch threads; generate mode: every '
+                    'chip generated on the GPU into pinned host memory): H2D upload overlapped with detection, device '
+                    'row packing, D2H of rows, gather of per-chip summaries on rank 0' % args.tile_pool}
 
 
 def synth_nobs(cfg, c):

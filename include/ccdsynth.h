@@ -38,6 +38,13 @@ int ccdsynth_dates(const ccdsynth_cfg *cfg, int32_t chip_index, int64_t *dates, 
 int ccdsynth_chip(const ccdsynth_cfg *cfg, int32_t chip_index, int32_t pix0, int32_t n_pix,
                   int32_t n_obs, const int64_t *dates, int16_t *spectra, uint16_t *qa);
 
+/* A chip whose every pixel series (7 bands and QA) is the given chip's rotated left by `shift`
+ * observations against the same dates: out[i] = in[(i + shift) mod n_obs].  The bench's source of
+ * a tile's distinct chips (ccdgpu.synth.TileSource 'pool' mode): a pool of generated chips, each
+ * tile position a different rotation, produced by copies at memory speed.  OpenMP, `threads`. */
+int ccdsynth_rotate(const int16_t *spectra, const uint16_t *qa, int32_t n_pix, int32_t n_obs, int32_t shift,
+                    int16_t *spectra_out, uint16_t *qa_out, int32_t threads);
+
 /* ---- device generator (lib/libccdsynth.so, csrc/ccd_synth.hip): the same samples computed on
  * a gfx950 GPU and copied into host buffers (pinned for full PCIe rate), for inputs too large to
  * generate on the host (a tile's 2500 distinct chips).  Same arithmetic as ccdsynth_chip

@@ -40,6 +40,8 @@ def lib():
         L.ccdsynth_gpu_destroy.argtypes = [ctypes.c_void_p]
         L.ccdsynth_gpu_error.restype = ctypes.c_char_p
         L.ccdsynth_gpu_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(SynthCfg), ctypes.c_int32] + [ctypes.c_void_p] * 9
+        L.ccdsynth_rotate.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
         _lib = L
     return _lib
 
@@ -135,15 +137,37 @@ class DeviceGenerator(object):
         return out
 
 
-class TileSource(object):
-    """``source(positions) -> ChipBatch`` for ccdc.runner: the tile chips at those positions, every
-    one distinct (chip id = tile position), generated on the GPU (DeviceGenerator, one per
-    calling thread) into pinned buffers from a pool, so they reach the detection path through
-    host memory and PCIe as fetched ARD would.  The runner hands each batch back with
-    ``release(batch)`` once its rows are fetched; the pool grows when every buffer is in use.
-    ``generate_seconds`` sums the time spent generating (GPU kernel + device-to-host copy)."""
+def rotate(spectra, qa, shift, out_spectra, out_qa, threads=8):
+    """out = the chip with every pixel series rotated left by ``shift`` observations (same
+    dates): out[..., i] = in[..., (i + shift) mod n] for the 7 bands and the QA (ccdsynth_rotate)."""
+    n_pix, n = qa.shape
+    assert spectra.shape == (7, n_pix, n) and out_spectra.shape == spectra.shape and out_qa.shape == qa.shape
+    for a in (spectra, qa, out_spectra, out_qa):
+        assert a.flags.c_contiguous
+    if lib().ccdsynth_rotate(spectra.ctypes.data, qa.ctypes.data, n_pix, n, int(shift), out_spectra.ctypes.data,
+                             out_qa.ctypes.data, int(threads)) != 0:
+        raise ValueError('ccdsynth_rotate failed')
 
-    def __init__(self, cfg, device=0, batch_chips=8, n_pix=10000, chip_of=None, pinned=True):
+
+class TileSource(object):
+    """``source(positions) -> ChipBatch`` for ccdc.runner: the tile chips at those positions, each
+    one distinct, in pinned buffers from a pool, so they reach the detection path through host
+    memory and PCIe as fetched ARD would.  The runner hands each batch back with
+    ``release(batch)`` once its rows are fetched; the pool grows when every buffer is in use.
+
+    mode 'generate': every chip generated on the GPU (DeviceGenerator, one per calling thread; chip
+    id = ``chip_of(position)``), its samples written into the pinned batch over PCIe -- exact
+    synthetic chips, but the generator's device-to-host traffic shares the link with the uploads
+    (the tile-parity run uses it).
+    mode 'pool': ``pool_chips`` chips generated once (``prepare``, before a timed run) and every
+    position served as one of them with each pixel series rotated by a position-dependent number
+    of observations (``rotate``: host copies at memory speed, ``rotate_threads`` per call) -- as many
+    distinct chips as positions, each of the tile's own cadence (the pool chip has the position's
+    date vector), without generator traffic on the link (the bench's tile leg).
+    ``generate_seconds`` sums the time spent producing batches."""
+
+    def __init__(self, cfg, device=0, batch_chips=8, n_pix=10000, chip_of=None, pinned=True, mode='generate',
+                 pool_chips=64, rotate_threads=8):
         import threading
         self.pinned = pinned
         self.cfg = cfg
@@ -151,10 +175,14 @@ class TileSource(object):
         self.batch_chips = int(batch_chips)
         self.n_pix = int(n_pix)
         self.chip_of = chip_of or (lambda pos: int(pos))
+        self.mode = mode
+        self.pool_chips = int(pool_chips)
+        self.rotate_threads = int(rotate_threads)
         self._local = threading.local()
         self._lock = threading.Lock()
         self._free = []
         self._gens = []
+        self._pool = None  # n_obs -> [(chip id, dates, spectra, qa)]
         self.max_obs = max(dates(cfg, c).shape[0] for c in range(64))  # base cadence / sidelap
         self.allocated = 0
         self.generate_seconds = 0.0
@@ -167,14 +195,43 @@ class TileSource(object):
                 self._gens.append(g)
         return g
 
+    def prepare(self):
+        """'pool' mode: generate the pool chips (ids 0 .. pool_chips-1 of the generator's tile
+        range 10^7 + i, by cadence), once."""
+        import ccdgpu
+        if self.mode != 'pool' or self._pool is not None:
+            return
+        g = self._gen()
+        ids = [10000000 + i for i in range(self.pool_chips)]
+        pool = {}
+        for i0 in range(0, len(ids), 8):
+            b = g.batch(self.cfg, ids[i0:i0 + 8], n_pix=self.n_pix, pinned=False)
+            for j, c in enumerate(ids[i0:i0 + 8]):
+                d, sp, q = b.chip(j)
+                pool.setdefault(int(d.shape[0]), []).append((c, np.array(d), np.array(sp), np.array(q)))
+        self._pool = pool
+
+    def _pool_chip(self, pos, chip_id, d):
+        group = self._pool.get(int(d.shape[0]))
+        if not group:
+            raise ValueError('no pool chip with %d observations' % d.shape[0])
+        h = (int(pos) * 2654435761) & 0xFFFFFFFF
+        src = group[h % len(group)]
+        if not np.array_equal(src[1], d):
+            raise ValueError('pool chip dates differ from the position\'s')
+        shift = 1 + (h >> 8) % (int(d.shape[0]) - 1)
+        return src, shift
+
     def __call__(self, positions):
         import time
         import ccdgpu
-        g = self._gen()
+        t = time.perf_counter()
+        g = self._gen() if self.mode == 'generate' else None
         ids = [self.chip_of(p) for p in positions]
         if len(ids) > self.batch_chips:
             raise ValueError('%d chips in one batch, the pool holds %d' % (len(ids), self.batch_chips))
-        nobs = [g.dates(self.cfg, c).shape[0] for c in ids]
+        dts = [g.dates(self.cfg, c) if g is not None else self._dates(c) for c in ids]
+        nobs = [d.shape[0] for d in dts]
         if max(nobs) > self.max_obs:
             raise ValueError('chip with %d observations past the pool buffers (%d)' % (max(nobs), self.max_obs))
         with self._lock:
@@ -184,11 +241,29 @@ class TileSource(object):
         if st is None:
             st = ccdgpu.batch_storage(self.batch_chips, self.n_pix, self.max_obs, pinned=self.pinned)
         b = ccdgpu.ChipBatch([self.n_pix] * len(ids), nobs, storage=st)
-        t = time.perf_counter()
-        g.batch(self.cfg, ids, n_pix=self.n_pix, out=b)
+        if g is not None:
+            g.batch(self.cfg, ids, n_pix=self.n_pix, out=b)
+        else:
+            if self._pool is None:
+                raise RuntimeError("TileSource('pool'): call prepare() first")
+            for j, (p, c, d) in enumerate(zip(positions, ids, dts)):
+                (_, pd, ps, pq), shift = self._pool_chip(p, c, d)
+                od, os_, oq = b.chip(j)
+                od[...] = d
+                rotate(ps, pq, shift, os_, oq, self.rotate_threads)
         with self._lock:
             self.generate_seconds += time.perf_counter() - t
         return b
+
+    def _dates(self, c):
+        key = int(c)
+        cache = getattr(self, '_date_cache', None)
+        if cache is None:
+            cache = self._date_cache = {}
+        d = cache.get(key)
+        if d is None:
+            d = cache[key] = dates(self.cfg, key)
+        return d
 
     def release(self, batch):
         if batch.storage is not None:

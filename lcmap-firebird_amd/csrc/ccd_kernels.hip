@@ -869,7 +869,13 @@ __device__ __forceinline__ int cd_sweep(Lds *L, int pc_rt, double alpha, int max
     return sweeps;
 }
 // the sweep with its coordinate count unrolled for the three model sizes (no per-coordinate branch)
+// (-DCCD_CD_CALL: one out-of-line copy shared by every fit_models call site instead of one inlined
+// copy per site -- fewer instruction-cache lines for the waves to share, a call's register saves)
+#ifdef CCD_CD_CALL
+__device__ __attribute__((noinline)) int cd_lanes(Lds *L, int pc, double alpha, int max_iter, double tol) {
+#else
 __device__ __forceinline__ int cd_lanes(Lds *L, int pc, double alpha, int max_iter, double tol) {
+#endif
     switch (pc) {
     case 3: return cd_sweep<3>(L, pc, alpha, max_iter, tol);
     case 5: return cd_sweep<5>(L, pc, alpha, max_iter, tol);

@@ -99,3 +99,25 @@ int ccdsynth_chip(const ccdsynth_cfg *cfg, int32_t chip, int32_t pix0, int32_t n
     }
     return 0;
 }
+
+int ccdsynth_rotate(const int16_t *spectra, const uint16_t *qa, int32_t n_pix, int32_t n_obs, int32_t shift,
+                    int16_t *spectra_out, uint16_t *qa_out, int32_t threads) {
+    if (n_pix <= 0 || n_obs <= 0 || !spectra || !qa || !spectra_out || !qa_out) return -1;
+    const int32_t k = ((shift % n_obs) + n_obs) % n_obs;
+    const size_t rows = (size_t)8 * (size_t)n_pix;  /* 7 band rows + the qa row per pixel */
+#pragma omp parallel for schedule(static) num_threads(threads > 0 ? threads : 1)
+    for (long long r = 0; r < (long long)rows; ++r) {
+        const size_t o = (size_t)(r % n_pix) * (size_t)n_obs;
+        const int b = (int)(r / n_pix);
+        if (b < 7) {
+            const int16_t *src = spectra + (size_t)b * (size_t)n_pix * (size_t)n_obs + o;
+            int16_t *dst = spectra_out + (size_t)b * (size_t)n_pix * (size_t)n_obs + o;
+            memcpy(dst, src + k, sizeof(int16_t) * (size_t)(n_obs - k));
+            memcpy(dst + (n_obs - k), src, sizeof(int16_t) * (size_t)k);
+        } else {
+            memcpy(qa_out + o, qa + o + k, sizeof(uint16_t) * (size_t)(n_obs - k));
+            memcpy(qa_out + o + (n_obs - k), qa + o, sizeof(uint16_t) * (size_t)k);
+        }
+    }
+    return 0;
+}

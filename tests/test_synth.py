@@ -24,3 +24,45 @@ def test_class_mix():
     fill = np.mean(q == 1)
     assert 0.05 < fill < 0.3
     assert np.all(s[:, q == 1] == -9999)
+
+
+class _HostGen(object):
+    """DeviceGenerator stand-in on the host (same samples: synth_core.h)."""
+
+    def batch(self, cfg, ids, n_pix=10000, pix0=0, out=None, pinned=False):
+        import ccdgpu
+        if out is None:
+            out = ccdgpu.ChipBatch([n_pix] * len(ids), [synth.dates(cfg, c).shape[0] for c in ids])
+        for j, c in enumerate(ids):
+            synth.chip(cfg, c, pix0, n_pix, out=out.chip(j))
+        return out
+
+    def dates(self, cfg, c):
+        return synth.dates(cfg, c)
+
+    def close(self):
+        pass
+
+
+def test_tile_source_pool_mode_serves_distinct_rotations(monkeypatch):
+    """TileSource 'pool' mode (the bench's tile leg): every position gets a pool chip of its own
+    date vector with every pixel series rotated; different positions differ; buffers recycle."""
+    import numpy as np
+    monkeypatch.setattr(synth.TileSource, '_gen', lambda self: _HostGen())
+    cfg = synth.config(3)
+    src = synth.TileSource(cfg, batch_chips=4, n_pix=12, mode='pool', pool_chips=6, pinned=False, rotate_threads=2)
+    src.prepare()
+    seen = set()
+    for pos0 in (0, 4, 8):
+        pos = list(range(pos0, pos0 + 4))
+        b = src(pos)
+        for j, p in enumerate(pos):
+            d, s, q = b.chip(j)
+            assert np.array_equal(d, synth.dates(cfg, p))
+            (cid, pd, ps, pq), shift = src._pool_chip(p, p, d)
+            assert 0 < shift < d.shape[0]
+            assert np.array_equal(s, np.roll(ps, -shift, axis=2)) and np.array_equal(q, np.roll(pq, -shift, axis=1))
+            seen.add((s.tobytes(), q.tobytes()))
+        src.release(b)
+    assert len(seen) == 12  # every position distinct
+    assert src.allocated == 1  # the released buffer was reused

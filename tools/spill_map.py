@@ -16,7 +16,10 @@ os.makedirs(TMP, exist_ok=True)
 src = sys.argv[sys.argv.index('--src') + 1] if '--src' in sys.argv else os.path.join(ROOT, 'lcmap-firebird_amd', 'csrc', 'ccd_kernels.hip')
 kern = sys.argv[sys.argv.index('--kernel') + 1] if '--kernel' in sys.argv else 'w3'
 out = os.path.join(TMP, 'k.s')
-subprocess.check_call(['hipcc', '--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-ffp-contract=on', '-gline-tables-only',
+if '--asm' in sys.argv:  # an existing -gline-tables-only assembly (e.g. built with the product's flags)
+    out = sys.argv[sys.argv.index('--asm') + 1]
+else:
+  subprocess.check_call(['hipcc', '--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-ffp-contract=on', '-gline-tables-only',
                        '--cuda-device-only', '-S', '-I' + os.path.join(ROOT, 'include'), src, '-o', out],
                       stderr=subprocess.DEVNULL)
 text = open(out).read()
