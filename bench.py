@@ -69,10 +69,12 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-packer', action='store_true', help='skip the chip-packer (chipmunk decode) leg')
     ap.add_argument('--tile-chips', type=int, default=TILE_CHIPS, help='chips of the headline tile leg per rank')
+    ap.add_argument('--no-resident', action='store_true',
+                    help='tile leg only (knob sweeps): no resident leg, roofline null, no CPU baselines')
     ap.add_argument('--no-tile', action='store_true',
                     help='resident leg only (kernel A/B runs): value = the resident rate, not the headline metric')
     ap.add_argument('--tile-batch', type=int, default=8, help='chips per launch in the tile leg')
-    ap.add_argument('--tile-pool', type=int, default=64, help='generated chips behind the tile leg\'s rotated chips')
+    ap.add_argument('--tile-pool', type=int, default=32, help='generated chips behind the tile leg\'s chips (each position a date-shifted copy)')
     ap.add_argument('--tile-contexts', type=int, default=2, help='contexts per GPU in the tile leg')
     ap.add_argument('--tile-depth', type=int, default=2, help='batches each tile-leg context keeps uploaded ahead')
     ap.add_argument('--share-device', action='store_true',
@@ -165,6 +167,18 @@ def main():
     device = local % ndev
     n_devices = min(world, ndev) if args.share_device else world
 
+    if args.no_resident:
+        tl = tile_leg(args, cfg, rank, world, device, dist)
+        if rank == 0:
+            print(json.dumps({'metric': 'tile leg only (knob sweep)', 'value': tl['value'], 'unit': 'pixels/s',
+                              'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': tl['ms_per_step'],
+                              'tile': tl, 'knobs': {'tile_batch': args.tile_batch, 'tile_contexts': args.tile_contexts,
+                                                    'tile_depth': args.tile_depth,
+                                                    'HSA_ENABLE_SDMA': os.environ.get('HSA_ENABLE_SDMA')}}),
+                  file=json_out, flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
     res = resident_leg(args, cfg, rank, world, device, dist)
     if args.no_tile:
         if rank == 0:
@@ -401,8 +415,8 @@ def tile_leg(args, cfg, rank, world, device, dist):
     src = synth.TileSource(cfg, device=device, batch_chips=B, mode=mode, pool_chips=args.tile_pool)
     t_prep = time.perf_counter()
     src.prepare()
-    # pinned batches in flight per context: depth + 1 staged, one fetched and waiting, one being fetched
-    src.prefill(args.tile_contexts * (args.tile_depth + 3))
+    # pinned batches in flight per context: depth + 1 (fetched or staged; the runner's slot permits)
+    src.prefill(args.tile_contexts * (args.tile_depth + 1) + 1)
     prep_s = time.perf_counter() - t_prep
     src_timed = src_warm = src
     ctxs = [ccdgpu.Context(device) for _ in range(args.tile_contexts)]
@@ -458,11 +472,11 @@ def tile_leg(args, cfg, rank, world, device, dist):
             'generate_seconds_rank0': round(gen_s, 3),
             'pinned_pool_batches': src_timed.allocated,
             'worker_seconds_rank0': {k: round(v, 3) for k, v in ranks[0].items() if k.endswith('_seconds')},
-            'note': 'ccdc.runner tile driver over distinct chips (pool mode: %d GPU-generated chips, each tile position '
-                    'one of them with every pixel series rotated by a position-dependent number of observations, '
-                    'produced by host copies into pinned batches in the runner\'s fetch threads; generate mode: every '
-                    'chip generated on the GPU into pinned host memory): H2D upload overlapped with detection, device '
-                    'row packing, D2H of rows, gather of per-chip summaries on rank 0' % args.tile_pool}
+            'note': 'ccdc.runner tile driver over distinct chip inputs (pool mode: %d GPU-generated chips generated before '
+                    'the timed run, each tile position a copy of one of its cadence with the acquisition dates moved by a '
+                    'position-dependent multiple of 16 days, copied into pinned batches by the runner\'s fetch threads; '
+                    'generate mode: every chip generated on the GPU into pinned host memory): H2D upload overlapped with '
+                    'detection, device row packing, D2H of rows, gather of per-chip summaries on rank 0' % args.tile_pool}
 
 
 def synth_nobs(cfg, c):

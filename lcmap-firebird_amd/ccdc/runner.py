@@ -142,15 +142,19 @@ def _pull_size(queue, batch_chips, tail_chips):
     return batch_chips
 
 
-def _fetcher(queue, source, batch_chips, tail_chips, stats, ready, stop):
+def _fetcher(queue, source, batch_chips, tail_chips, stats, ready, stop, permits):
     """A worker's fetch thread: pulls the next positions from the shared queue and asks the source
     for their ARD (the merlin / chipmunk fetch stand-in; often I/O- or copy-bound), so the fetch
     of the next batches overlaps the upload, detection and row fetch of the current ones.  Puts
-    (positions, batch) on ``ready`` (bounded: one batch waits while the next is fetched), then
-    None when the queue is empty, or the exception that stopped it."""
+    (positions, batch) on ``ready``, then None when the queue is empty, or the exception that
+    stopped it.  A fetch starts only with one of the worker's upload-slot ``permits`` (a slot
+    that is free or will be by the time the batch arrives), so at most depth + 1 batches of a
+    worker are fetched or staged at once -- the source's buffers stay bounded."""
     clock = time.perf_counter
     try:
         while not stop.is_set():
+            if not permits.acquire(timeout=0.1):
+                continue
             t0 = clock()
             pos = queue.next(_pull_size(queue, batch_chips, tail_chips))
             if not pos:
@@ -175,9 +179,11 @@ def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, er
     are past their upload).  The ARD of the next batches is fetched by the worker's own fetch
     thread (``_fetcher``) meanwhile.  Near the end of the queue the batches shrink (``_pull_size``)."""
     import queue as queue_mod
-    ready = queue_mod.Queue(maxsize=1)  # one fetched batch waiting (+ one being fetched)
+    ready = queue_mod.Queue()
     stop = threading.Event()
-    ft = threading.Thread(target=_fetcher, args=(queue, source, batch_chips, tail_chips, stats, ready, stop), daemon=True)
+    permits = threading.Semaphore(depth + 1)  # one per upload slot
+    ft = threading.Thread(target=_fetcher, args=(queue, source, batch_chips, tail_chips, stats, ready, stop, permits),
+                          daemon=True)
     ft.start()
     try:
         clock = time.perf_counter
@@ -216,6 +222,7 @@ def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, er
             cy = np.array([xys[p][1] for p in ppos], dtype=np.int32)
             off, rows, mask = ctx.fetch_batch_rows(cx, cy, width)
             free.append(s)  # its rows are fetched: the slot takes the next upload
+            permits.release()
             t4 = clock()
             for c, p in enumerate(ppos):
                 p0, p1 = int(pbatch.pix_off[c]), int(pbatch.pix_off[c + 1])

@@ -160,10 +160,12 @@ class TileSource(object):
     synthetic chips, but the generator's device-to-host traffic shares the link with the uploads
     (the tile-parity run uses it).
     mode 'pool': ``pool_chips`` chips generated once (``prepare``, before a timed run) and every
-    position served as one of them with each pixel series rotated by a position-dependent number
-    of observations (``rotate``: host copies at memory speed, ``rotate_threads`` per call) -- as many
-    distinct chips as positions, each of the tile's own cadence (the pool chip has the position's
-    date vector), without generator traffic on the link (the bench's tile leg).
+    position served as a copy of one of them (of the position's own cadence) with its acquisition
+    dates moved later by a position-dependent multiple of 16 days (one Landsat repeat cycle, so
+    the cadence pattern is kept): every position a distinct (dates, ARD) input whose detection
+    genuinely differs (the trend term and the harmonics see other dates), with the statistics of
+    a generated chip, produced by host copies at memory speed (``rotate_threads`` per call) and
+    without generator traffic on the PCIe link (the bench's tile leg).
     ``generate_seconds`` sums the time spent producing batches."""
 
     def __init__(self, cfg, device=0, batch_chips=8, n_pix=10000, chip_of=None, pinned=True, mode='generate',
@@ -212,6 +214,7 @@ class TileSource(object):
         self._pool = pool
 
     def _pool_chip(self, pos, chip_id, d):
+        """(pool chip, date shift in days) serving position ``pos`` (its chip's dates ``d``)."""
         group = self._pool.get(int(d.shape[0]))
         if not group:
             raise ValueError('no pool chip with %d observations' % d.shape[0])
@@ -219,8 +222,7 @@ class TileSource(object):
         src = group[h % len(group)]
         if not np.array_equal(src[1], d):
             raise ValueError('pool chip dates differ from the position\'s')
-        shift = 1 + (h >> 8) % (int(d.shape[0]) - 1)
-        return src, shift
+        return src, 16 * (1 + (h >> 8) % 64)
 
     def __call__(self, positions):
         import time
@@ -247,10 +249,10 @@ class TileSource(object):
             if self._pool is None:
                 raise RuntimeError("TileSource('pool'): call prepare() first")
             for j, (p, c, d) in enumerate(zip(positions, ids, dts)):
-                (_, pd, ps, pq), shift = self._pool_chip(p, c, d)
+                (_, pd, ps, pq), days = self._pool_chip(p, c, d)
                 od, os_, oq = b.chip(j)
-                od[...] = d
-                rotate(ps, pq, shift, os_, oq, self.rotate_threads)
+                od[...] = pd + days
+                rotate(ps, pq, 0, os_, oq, self.rotate_threads)  # (shift 0: a parallel copy)
         with self._lock:
             self.generate_seconds += time.perf_counter() - t
         return b

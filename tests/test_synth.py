@@ -44,9 +44,10 @@ class _HostGen(object):
         pass
 
 
-def test_tile_source_pool_mode_serves_distinct_rotations(monkeypatch):
-    """TileSource 'pool' mode (the bench's tile leg): every position gets a pool chip of its own
-    date vector with every pixel series rotated; different positions differ; buffers recycle."""
+def test_tile_source_pool_mode_serves_distinct_chips(monkeypatch):
+    """TileSource 'pool' mode (the bench's tile leg): every position gets a copy of a pool chip of
+    its own cadence with its dates moved by a multiple of 16 days; positions differ; buffers
+    recycle."""
     import numpy as np
     monkeypatch.setattr(synth.TileSource, '_gen', lambda self: _HostGen())
     cfg = synth.config(3)
@@ -58,11 +59,12 @@ def test_tile_source_pool_mode_serves_distinct_rotations(monkeypatch):
         b = src(pos)
         for j, p in enumerate(pos):
             d, s, q = b.chip(j)
-            assert np.array_equal(d, synth.dates(cfg, p))
-            (cid, pd, ps, pq), shift = src._pool_chip(p, p, d)
-            assert 0 < shift < d.shape[0]
-            assert np.array_equal(s, np.roll(ps, -shift, axis=2)) and np.array_equal(q, np.roll(pq, -shift, axis=1))
-            seen.add((s.tobytes(), q.tobytes()))
+            d0 = synth.dates(cfg, p)
+            (cid, pd, ps, pq), days = src._pool_chip(p, p, d0)
+            assert days % 16 == 0 and 16 <= days <= 1024
+            assert np.array_equal(d, d0 + days) and np.array_equal(pd, d0)
+            assert np.array_equal(s, ps) and np.array_equal(q, pq)
+            seen.add((cid, d.tobytes()))
         src.release(b)
     assert len(seen) == 12  # every position distinct
     assert src.allocated == 1  # the released buffer was reused

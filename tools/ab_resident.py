@@ -30,15 +30,18 @@ ids = bench.chip_ids(0, a.chips, 1, lambda c: bench.synth_nobs(cfg, c))
 batch = bench.build_batch(cfg, ids)
 res = {}
 for r in range(a.rounds):
-    for path in a.libs:
+    for spec in a.libs:
+        # "lib.so:w4" runs the library's 4-waves/SIMD kernel (CCDGPU_KERNEL, read at context creation)
+        path, _, variant = spec.partition(':')
+        os.environ['CCDGPU_KERNEL'] = variant or 'w3'
         ccdgpu._lib = None
         ccdgpu.LIB_PATH = path if os.path.isabs(path) else os.path.join(ROOT, 'lcmap-firebird_amd', path)
         ns = argparse.Namespace(chips=a.chips, contexts=a.contexts, warmup=a.warmup, steps=a.steps, config=a.config)
         out = bench.resident_leg(ns, cfg, 0, 1, 0, None, batch=batch)
         rate = out['value']
-        res.setdefault(path, []).append({'value': rate, 'frac': out['roofline']['frac'],
+        res.setdefault(spec, []).append({'value': rate, 'frac': out['roofline']['frac'],
                                          'kernel_ms': out['roofline']['kernel_ms_per_launch']})
         print('C%d %-40s round %d  %.0f px/s  frac %.4f  kernel %.1f ms' % (
-            a.config, os.path.basename(path), r, rate, out['roofline']['frac'], out['roofline']['kernel_ms_per_launch']),
+            a.config, os.path.basename(spec), r, rate, out['roofline']['frac'], out['roofline']['kernel_ms_per_launch']),
             flush=True)
 print(json.dumps({'config': a.config, 'chips': a.chips, 'workload_key': out['workload_key'], 'results': res}))

@@ -3,7 +3,7 @@
 # Each pass is SIGKILL-bounded: a counter request the hardware cannot hold hangs rocprofv3.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; OUT="$R/gpurun_out"; mkdir -p "$OUT"; TAG=${1:-pmc}
-CMD="python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-packer --no-tile --chips ${CHIPS:-64} --contexts 1"
+CMD="python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-packer --no-tile --chips ${CHIPS:-64} --contexts 1 --config ${CONFIG:-3}"
 cd /tmp && export TMPDIR=/tmp
 i=0
 for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
