@@ -76,6 +76,7 @@ def parse():
     ap.add_argument('--tile-batch', type=int, default=8, help='chips per launch in the tile leg')
     ap.add_argument('--tile-pool', type=int, default=32, help='generated chips behind the tile leg\'s chips (each position a date-shifted copy)')
     ap.add_argument('--tile-contexts', type=int, default=2, help='contexts per GPU in the tile leg')
+    ap.add_argument('--tile-copy-threads', type=int, default=8, help='host threads per pool-chip copy in the tile leg source')
     ap.add_argument('--tile-depth', type=int, default=2, help='batches each tile-leg context keeps uploaded ahead')
     ap.add_argument('--share-device', action='store_true',
                     help='rehearsal only: ranks beyond the device count share devices (LOCAL_RANK mod count)')
@@ -412,7 +413,8 @@ def tile_leg(args, cfg, rank, world, device, dist):
     # (configs 3 / 5, whose chips share two date vectors); configs 2 / 4 subsample dates per chip,
     # so there every chip is generated on the GPU
     mode = 'pool' if args.config in (3, 5) else 'generate'
-    src = synth.TileSource(cfg, device=device, batch_chips=B, mode=mode, pool_chips=args.tile_pool)
+    src = synth.TileSource(cfg, device=device, batch_chips=B, mode=mode, pool_chips=args.tile_pool,
+                           rotate_threads=args.tile_copy_threads)
     t_prep = time.perf_counter()
     src.prepare()
     # pinned batches in flight per context: depth + 1 (fetched or staged; the runner's slot permits)
@@ -468,6 +470,7 @@ def tile_leg(args, cfg, rank, world, device, dist):
             'chips_per_rank_done': {r: st['chips'] for r, st in ranks.items()},
             'tail_seconds_per_rank': {r: round(st.get('tail_seconds', 0.0), 3) for r, st in ranks.items()},
             'source_mode': mode, 'source_pool_chips': args.tile_pool if mode == 'pool' else None,
+            'source_copy_threads': args.tile_copy_threads if mode == 'pool' else None,
             'source_prepare_seconds': round(prep_s, 2),
             'generate_seconds_rank0': round(gen_s, 3),
             'pinned_pool_batches': src_timed.allocated,

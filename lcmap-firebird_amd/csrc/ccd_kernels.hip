@@ -725,6 +725,22 @@ __device__ __forceinline__ float gmax8f(float v XL) {
     return r;
 }
 
+// gmax8f of two values at once: the two reductions' DPP maxima interleaved, so each level's
+// second operation supplies one of the two wait states the next level's DPP read needs
+__device__ __forceinline__ void gmax8f2(float u, float v, float &ru, float &rv XL) {
+    EXEC_FULL();
+    asm("s_nop 1\n\t"
+        "v_max_f32_dpp %0, %2, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_max_f32_dpp %1, %3, %3 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 0\n\t"
+        "v_max_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_max_f32_dpp %1, %1, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 0\n\t"
+        "v_max_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "v_max_f32_dpp %1, %1, %1 row_half_mirror row_mask:0xf bank_mask:0xf"
+        : "=&v"(ru), "=&v"(rv) : "v"(u), "v"(v));
+}
+
 // One coordinate of the cyclic sweep (coordinate J of every band group).  Lane (b, k) holds
 // h_k = g_k + G_kk w_k, where g_k = q_k - sum_m G_km w_m is the correlation X_k . R of sklearn's
 // residual form: h_J is sklearn's tmp = X_J . (R + w_J X_J) for coordinate J as it stands, so the
@@ -814,8 +830,8 @@ __device__ __forceinline__ int cd_sweep(Lds *L, int pc_rt, double alpha, int max
         // below ~1e-8 (or flushed denormals) tw can be subnormal, so tw < 2^-125 also goes exact.
         unsigned long long rl, wz = 0ull;  // groups with d_w_max / w_max < tol, with w_max = 0
         {
-            const float D = gmax8f((float)fabs(w - w0));
-            const float Wf = gmax8f((float)fabs(w));  // w stays 0 in lanes outside the model
+            float D, Wf;  // w stays 0 in lanes outside the model
+            gmax8f2((float)fabs(w - w0), (float)fabs(w), D, Wf);
             const float tw = tol_f * Wf;
             // (one ballot per comparison: each v_cmp writes its lane mask straight to SGPRs)
             const unsigned long long wokm = bal(Wf >= 0x1p-100f) & bal(Wf <= 0x1p100f) & bal(tw >= 0x1p-125f);
@@ -2019,6 +2035,7 @@ __device__ __forceinline__ bool initialize(Px &P, int &wa, int &wb) {
         PH_BEGIN(tm)
         const int cnt = tmask(P, a, b);
         PH_END(P, tm, 3)
+        PH_COUNT(P, 32, 1)
         const int nw = b - a;
         if (cnt == nw) { b += 1; continue; }
         // first / last kept observation of the window
@@ -2041,6 +2058,7 @@ __device__ __forceinline__ bool initialize(Px &P, int &wa, int &wb) {
             b -= cnt;
         }
         fit_models(P, a, b, 4);
+        PH_COUNT(P, 33, 1)
         count_stable(P);
         PH_BEGIN(st)
         const bool stb = stable(P, a, b);
@@ -2685,8 +2703,16 @@ __device__ __forceinline__ void spec_fits(Px &P, int a, int nw0, int V, SpecFit 
     const bool any5 = bal(act && pc > 3) != 0ull;
     bool done = !act;
     int sweeps = max_iter;
+#ifdef CCD_PHASE_TIMERS
+    int wave_sweeps = max_iter;
+#endif
     for (int it = 0; it < max_iter; ++it) {
-        if (bal(!done) == 0ull) break;
+        if (bal(!done) == 0ull) {
+#ifdef CCD_PHASE_TIMERS
+            wave_sweeps = it;
+#endif
+            break;
+        }
         double dmax = 0.0;
 #pragma unroll
         for (int i = 0; i < SPEC_PC; ++i) {
@@ -2748,6 +2774,16 @@ __device__ __forceinline__ void spec_fits(Px &P, int a, int nw0, int V, SpecFit 
         ss += res * res;
     }
     wsync();  // the row tile is free again (the replay's peek residuals go there)
+#ifdef CCD_PHASE_TIMERS
+    {
+        int ls = act ? sweeps : 0;  // lane sweeps summed over the active lanes
+        for (int o = 32; o > 0; o >>= 1) ls += shfx(ls, o);
+        PH_COUNT(P, 35, 1)
+        PH_COUNT(P, 36, V)
+        PH_COUNT(P, 38, wave_sweeps)
+        PH_COUNT(P, 39, ls)
+    }
+#endif
 #pragma unroll
     for (int i = 0; i < SPEC_PC; ++i) F.w[i] = w[i];
     F.c = c;
@@ -2825,9 +2861,27 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
     int moff = 0;            // ring offset of the last evaluated peek window
     int hfa = -1, hfb = -1;  // fit window the closest-DOY buckets describe
     int nc_fit = nc;         // coefficients of the current fit
+    // One fit_models site for the three refits of this loop (an early step, the long-peek span
+    // refit, the batched span refit): a path that needs a fit records it in fmode and continues,
+    // the fit runs at the top of the next iteration, and the early / long-peek steps then resume
+    // with their single-step evaluation (ev), which they share.  One inlined copy of the Gram +
+    // coordinate descent instead of three keeps the kernel body (and its instruction-cache
+    // footprint) smaller; the order of operations is unchanged.
+    int fmode = 0;  // pending fit: 1 early step, 2 long-peek span refit, 3 batched refit
     for (;;) {
-        if (!(b + k < P.m || !have)) break;
-        if (!have || b - a < 24) {
+        int ev = 0;  // single-step evaluation of this iteration: 1 early step, 2 long peek
+        if (fmode) {
+            fit_models(P, fa, fb, nc_fit, fmode == 1 || fb - fa <= 24);  // rmse: from build_closest when it runs
+            if (fmode == 1) {
+                have = true;
+                if (l < NB) L->comp[l] = L->rmse[l];  // early step: comparison rmse = model rmse
+                wsync();
+            }
+            ev = fmode == 3 ? 0 : fmode;
+            fmode = 0;
+        }
+        if (!ev && !(b + k < P.m || !have)) break;
+        if (!ev && (!have || b - a < 24)) {
             // early steps: speculative fits of the next windows, then the steps one by one
             const int nw0 = b - a;
             int V = 24 - nw0;
@@ -2853,6 +2907,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
                     if (installed != sp) {
                         spec_install(P, F, sp, b - a, nc);
                         installed = sp;
+                        PH_COUNT(P, 37, 1)
                     }
                     nc_fit = nc;
                     have = true;
@@ -2878,56 +2933,46 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
                 if (brk) break;
                 continue;
             }
-            // early step: refit every step, comparison rmse = model rmse
+            // early step: refit every step (comparison rmse = model rmse), then evaluate it
             nc = num_coefs(p, b - a);
             peek_start = b;
             fa = a;
             fb = b;
             fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
-            fit_models(P, fa, fb, nc);
             nc_fit = nc;
-            have = true;
-            if (l < NB) L->comp[l] = L->rmse[l];
-            wsync();
-            double m0;
-            PH_BEGIN(ep)
-            const bool chg_now = eval_peek(P, k, b, 1, m0);
-            PH_END(P, ep, 8)
-            moff = 0;
-            if (chg_now) {
-                change = 1.0;
-                break;
-            }
-            if (m0 > p.outlier_threshold) {
-                const int rm = b;
-                compact_drop(P, rm, rm + 1, [&](int j) { return j == rm; });
-                continue;
-            }
-            b += 1;
+            fmode = 1;
             continue;
         }
-        if (k > W) {
+        if (!ev && k > W) {
             // A peek longer than the 64-row ring (adaptive peek > 64: median date gap < 1.5
             // days) runs one step at a time in change.lookforward's own order: refit on the span
             // test, comparison rmse from the 24 closest-DOY fit observations of the peek end.
             nc = num_coefs(p, b - a);
             peek_start = b;
             const double span = (double)CDR(P, b - 1) - (double)CDR(P, a);
+            ev = 2;
             if (span >= 1.33 * fit_span) {
                 fa = a;
                 fb = b;
                 fit_span = span;
-                fit_models(P, fa, fb, nc, fb - fa <= 24);
                 nc_fit = nc;
+                fmode = 2;
+                continue;
             }
-            if (fb - fa > 24 && (hfa != fa || hfb != fb)) {
-                build_closest(P, fa, fb, nc_fit);
-                hfa = fa;
-                hfb = fb;
+        }
+        if (ev) {
+            if (ev == 2) {
+                if (fb - fa > 24 && (hfa != fa || hfb != fb)) {
+                    build_closest(P, fa, fb, nc_fit);
+                    hfa = fa;
+                    hfb = fb;
+                }
+                closest_doy_scan(P, fa, fb, b + k - 1);
             }
-            closest_doy_scan(P, fa, fb, b + k - 1);
             double m0;
+            PH_BEGIN(ep)
             const bool chg_now = eval_peek(P, k, b, 1, m0);
+            PH_END(P, ep, 8)
             moff = 0;
             if (chg_now) {
                 change = 1.0;
@@ -3060,8 +3105,9 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
             fa = a;
             fb = b;
             fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
-            fit_models(P, fa, fb, nc, fb - fa <= 24);  // rmse: from build_closest when it runs
             nc_fit = nc;
+            fmode = 3;  // the refit runs at the top of the loop
+            PH_COUNT(P, 34, 1)
         }
     }
     PH_BEGIN(md)
@@ -3082,23 +3128,55 @@ __device__ __forceinline__ void standard_procedure(Px &P) {
     PH_END(P, vg, 2)
     int a = 0, b = meow, prev = 0, nres = 0;
     bool start = true;
-    while (b <= P.m - meow) {
-        if (nres > 0) start = false;
-        if (!initialize(P, a, b)) break;
-        if (a > prev) lookback(P, a, b, prev);
-        if (a - prev > P.peek && start) {
-            catch_(P, prev, a, p.curve_qa_start);
-            nres++;
-            start = false;
+    // ccd.procedures.standard_procedure's loop with its two catch() calls (the start segment
+    // before a model, the end segment after the last one) run from one site (one inlined copy of
+    // the fit): cmode 1 = the start catch, after which the iteration resumes; 2 = the end catch.
+    int cmode = 0, ca = 0, cb = 0, cq = 0;
+    for (;;) {
+        bool resume = false;
+        if (cmode) {
+            catch_(P, ca, cb, cq);
+            if (cmode == 2) break;
+            cmode = 0;
+            resume = true;
         }
-        if (b + P.peek > P.m) break;
+        bool end = false;
+        if (!resume) {
+            if (!(b <= P.m - meow)) {
+                end = true;
+            } else {
+                if (nres > 0) start = false;
+                if (!initialize(P, a, b)) {
+                    end = true;
+                } else {
+                    if (a > prev) lookback(P, a, b, prev);
+                    if (a - prev > P.peek && start) {
+                        ca = prev;
+                        cb = a;
+                        cq = p.curve_qa_start;
+                        cmode = 1;
+                        nres++;
+                        start = false;
+                        continue;
+                    }
+                }
+            }
+        }
+        if (!end && b + P.peek > P.m) end = true;
+        if (end) {
+            if (!(prev + P.peek < P.m)) break;
+            ca = prev;
+            cb = P.m;
+            cq = p.curve_qa_end;
+            cmode = 2;
+            continue;
+        }
         lookforward(P, a, b);
         nres++;
         prev = b;
         a = b;
         b = b + meow;
     }
-    if (prev + P.peek < P.m) catch_(P, prev, P.m, p.curve_qa_end);
 }
 
 // ------------------------------------------------------------------ qa.py filters + compaction

@@ -10,8 +10,36 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#include <emmintrin.h>
 
 #include "synth_core.h"
+
+/* dst = src (n bytes) with streaming (non-temporal) 16-byte stores: the destination is a pinned
+ * upload buffer the CPU will not read again, so its lines are not fetched before being written
+ * (a plain copy of a few-KB row costs a read of the destination line per line written) */
+static void copy_stream(void *dst, const void *src, size_t n) {
+    char *d = (char *)dst;
+    const char *s = (const char *)src;
+    const size_t head = (16 - ((uintptr_t)d & 15)) & 15;
+    if (n < 64 + head) {
+        memcpy(d, s, n);
+        return;
+    }
+    memcpy(d, s, head);
+    d += head, s += head, n -= head;
+    size_t i = 0;
+    for (; i + 64 <= n; i += 64) {
+        const __m128i a = _mm_loadu_si128((const __m128i *)(s + i));
+        const __m128i b = _mm_loadu_si128((const __m128i *)(s + i + 16));
+        const __m128i c = _mm_loadu_si128((const __m128i *)(s + i + 32));
+        const __m128i e = _mm_loadu_si128((const __m128i *)(s + i + 48));
+        _mm_stream_si128((__m128i *)(d + i), a);
+        _mm_stream_si128((__m128i *)(d + i + 16), b);
+        _mm_stream_si128((__m128i *)(d + i + 32), c);
+        _mm_stream_si128((__m128i *)(d + i + 48), e);
+    }
+    memcpy(d + i, s + i, n - i);
+}
 
 int ccdsynth_config(int which, ccdsynth_cfg *c) {
     memset(c, 0, sizeof(*c));
@@ -104,6 +132,26 @@ int ccdsynth_rotate(const int16_t *spectra, const uint16_t *qa, int32_t n_pix, i
                     int16_t *spectra_out, uint16_t *qa_out, int32_t threads) {
     if (n_pix <= 0 || n_obs <= 0 || !spectra || !qa || !spectra_out || !qa_out) return -1;
     const int32_t k = ((shift % n_obs) + n_obs) % n_obs;
+    if (k == 0) {
+        /* a plain copy: both arrays in large contiguous pieces, one per thread, streamed */
+        const size_t ns = (size_t)7 * (size_t)n_pix * (size_t)n_obs * sizeof(int16_t);
+        const size_t nq = (size_t)n_pix * (size_t)n_obs * sizeof(uint16_t);
+        const int nt = threads > 0 ? threads : 1;
+        const size_t piece = ((ns + nq) / (size_t)nt + 4095) & ~(size_t)4095;
+#pragma omp parallel for schedule(static) num_threads(nt)
+        for (int t = 0; t < nt; ++t) {
+            size_t a = (size_t)t * piece, e = a + piece;
+            if (e > ns + nq) e = ns + nq;
+            if (a >= e) continue;
+            if (a < ns) copy_stream((char *)spectra_out + a, (const char *)spectra + a, (e < ns ? e : ns) - a);
+            if (e > ns) {
+                const size_t qa0 = a > ns ? a - ns : 0;
+                copy_stream((char *)qa_out + qa0, (const char *)qa + qa0, e - ns - qa0);
+            }
+            _mm_sfence();  /* this thread's streaming stores are visible before the upload reads them */
+        }
+        return 0;
+    }
     const size_t rows = (size_t)8 * (size_t)n_pix;  /* 7 band rows + the qa row per pixel */
 #pragma omp parallel for schedule(static) num_threads(threads > 0 ? threads : 1)
     for (long long r = 0; r < (long long)rows; ++r) {

@@ -33,6 +33,9 @@ for i, n in enumerate(['batches ne<=16', 'batches ne<=32', 'batch valid lanes', 
                        'wave fits at max_iter', 'wave sweeps (single fits)', 'wave sweeps in max_iter fits',
                        'compaction rows scanned']):
     out[n] = dc[8 + 24 + i]
+for i, n in enumerate(['init tmask calls', 'init fits', 'lf batched refits', 'spec calls', 'spec windows computed',
+                       'spec windows installed', 'spec wave sweeps', 'spec lane sweeps']):
+    out[n] = dc[8 + 32 + i]
 out['pixels'] = chips * 10000
 out['cycles_per_pixel'] = tot / out['pixels']
 print(json.dumps(out, indent=1))
