@@ -77,6 +77,7 @@ def parse():
     ap.add_argument('--tile-pool', type=int, default=32, help='generated chips behind the tile leg\'s chips (each position a date-shifted copy)')
     ap.add_argument('--tile-contexts', type=int, default=2, help='contexts per GPU in the tile leg')
     ap.add_argument('--tile-copy-threads', type=int, default=8, help='host threads per pool-chip copy in the tile leg source')
+    ap.add_argument('--tile-no-numa', action='store_true', help='tile leg: leave host threads unbound (A/B)')
     ap.add_argument('--tile-depth', type=int, default=2, help='batches each tile-leg context keeps uploaded ahead')
     ap.add_argument('--share-device', action='store_true',
                     help='rehearsal only: ranks beyond the device count share devices (LOCAL_RANK mod count)')
@@ -413,6 +414,12 @@ def tile_leg(args, cfg, rank, world, device, dist):
     # (configs 3 / 5, whose chips share two date vectors); configs 2 / 4 subsample dates per chip,
     # so there every chip is generated on the GPU
     mode = 'pool' if args.config in (3, 5) else 'generate'
+    # host threads and the pinned batches they fill on the GPU's NUMA node (as the runner does)
+    numa_node = None
+    if not args.tile_no_numa:
+        import ccdgpu as _cg
+        numa_node = _cg.device_numa_node(device)
+        runner.bind_to_device_node(device, numa_node)
     src = synth.TileSource(cfg, device=device, batch_chips=B, mode=mode, pool_chips=args.tile_pool,
                            rotate_threads=args.tile_copy_threads)
     t_prep = time.perf_counter()
@@ -437,7 +444,8 @@ def tile_leg(args, cfg, rank, world, device, dist):
         sink = runner.SummarySink(digest=False)
         xys = [xy(p) for p in range(n)]
         return runner.changedetection(xys, src, device=device, contexts=args.tile_contexts, batch_chips=B,
-                                      sink=sink, upload_depth=args.tile_depth, context_factory=factory)
+                                      sink=sink, upload_depth=args.tile_depth, context_factory=factory,
+                                      bind_numa=not args.tile_no_numa)
 
     if warm_total:
         run(warm_total, _Offset(src_warm, 1000000))
@@ -471,6 +479,7 @@ def tile_leg(args, cfg, rank, world, device, dist):
             'tail_seconds_per_rank': {r: round(st.get('tail_seconds', 0.0), 3) for r, st in ranks.items()},
             'source_mode': mode, 'source_pool_chips': args.tile_pool if mode == 'pool' else None,
             'source_copy_threads': args.tile_copy_threads if mode == 'pool' else None,
+            'gpu_numa_node': numa_node, 'host_threads_bound_to_gpu_node': not args.tile_no_numa,
             'source_prepare_seconds': round(prep_s, 2),
             'generate_seconds_rank0': round(gen_s, 3),
             'pinned_pool_batches': src_timed.allocated,

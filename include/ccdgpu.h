@@ -141,6 +141,11 @@ void ccdgpu_params_default(ccdgpu_params *p);
 int ccdgpu_init(int device, ccdgpu_ctx **ctx);
 int ccdgpu_destroy(ccdgpu_ctx *ctx);
 int ccdgpu_device_count(int *count);
+/* NUMA node of HIP device `device`'s PCIe attachment (sysfs numa_node of its bus id; -1 when the
+ * platform does not say).  The tile driver (ccdc.runner) keeps its host threads and pinned upload
+ * buffers on that node, so the chip copies and the DMA reads of them stay on the socket the GPU
+ * hangs off.  (No reference counterpart: Spark placed executors, ccdc/core.py:97-108.) */
+int ccdgpu_device_numa_node(int device, int *node);
 int ccdgpu_synchronize(ccdgpu_ctx *ctx);
 
 /* Host-buffer entry point (the pyccd.detect / ccd.detect path).

@@ -76,6 +76,56 @@ class StoreQueue(object):
         return max(0, self.total - int(self.store.add(self.key, 0)))
 
 
+# --------------------------------------------------------------------------- host placement
+def node_cpus(node):
+    """CPU ids of NUMA node ``node`` (sysfs cpulist), or None."""
+    try:
+        text = open('/sys/devices/system/node/node%d/cpulist' % int(node)).read().strip()
+    except (OSError, ValueError):
+        return None
+    cpus = set()
+    for part in text.split(','):
+        if '-' in part:
+            a, b = part.split('-')
+            cpus.update(range(int(a), int(b) + 1))
+        elif part:
+            cpus.add(int(part))
+    return cpus
+
+
+def bind_to_device_node(device, numa_node=None):
+    """Restrict the calling thread -- and every thread it starts afterwards (worker, fetch and
+    copy threads inherit it) -- to the CPUs of the NUMA node GPU ``device`` is attached to,
+    within the current affinity, so the host copies of chip data and the pinned buffers they
+    land in (first touched by those threads) sit on the socket the GPU's DMA reads from.
+    Returns the previous affinity (for restore_affinity), or None when the node is unknown or
+    the intersection is empty (nothing changed)."""
+    import os
+    if not hasattr(os, 'sched_getaffinity'):
+        return None
+    if numa_node is None:
+        try:
+            import ccdgpu
+            numa_node = ccdgpu.device_numa_node(device)
+        except Exception:  # no GPU runtime / device here: leave the placement alone
+            return None
+    if numa_node is None or numa_node < 0:
+        return None
+    cpus = node_cpus(numa_node)
+    old = os.sched_getaffinity(0)
+    want = (cpus or set()) & old
+    if not want or want == old:
+        return None
+    os.sched_setaffinity(0, want)
+    return old
+
+
+def restore_affinity(old):
+    import os
+    if old:
+        os.sched_setaffinity(0, old)
+
+
 # --------------------------------------------------------------------------- sinks
 def chip_checksum(row_offsets, rows, mask_bits):
     """Order-sensitive digest of one chip's rows and processing-mask bit words (for gathers and
@@ -254,7 +304,7 @@ def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, er
 
 
 def detect_tile(xys, source, queue, device=0, contexts=2, batch_chips=16, params=None, width=100,
-                sink=None, context_factory=None, upload_depth=2, tail_chips=None):
+                sink=None, context_factory=None, upload_depth=2, tail_chips=None, bind_numa=True):
     """Change detection of the tile chips at ``xys`` (list of (cx, cy), tile order) on one GPU.
 
     ``source(positions) -> ccdgpu.ChipBatch`` supplies the ARD of the chips at those tile
@@ -288,6 +338,8 @@ def detect_tile(xys, source, queue, device=0, contexts=2, batch_chips=16, params
              'queue_empty_at': 0.0}
     errors = []
     ctxs = [context_factory(device) for _ in range(max(1, int(contexts)))]
+    # worker / fetch / copy threads on the GPU's NUMA node (restored when the tile is done)
+    old_aff = bind_to_device_node(device) if bind_numa else None
     try:
         th = [threading.Thread(target=_worker, args=(c, queue, source, xys, int(batch_chips), params, width, sink, stats,
                                                        errors, int(upload_depth), int(tail_chips)))
@@ -299,6 +351,7 @@ def detect_tile(xys, source, queue, device=0, contexts=2, batch_chips=16, params
     finally:
         for c in ctxs:
             c.close()
+        restore_affinity(old_aff)
     stats.pop('lock')
     stats.pop('t0')
     stats['seconds'] = time.perf_counter() - t0
@@ -341,7 +394,8 @@ class TileError(RuntimeError):
 
 
 def changedetection(tile, source, device=None, contexts=2, batch_chips=16, number=None, params=None,
-                    sink=None, width=100, context_factory=None, ctx=None, upload_depth=2, tail_chips=None):
+                    sink=None, width=100, context_factory=None, ctx=None, upload_depth=2, tail_chips=None,
+                    bind_numa=True):
     """Change detection for a tile on every GPU of the job (reference core.changedetection,
     ccdc/core.py:78-123).
 
@@ -383,7 +437,7 @@ def changedetection(tile, source, device=None, contexts=2, batch_chips=16, numbe
     try:
         sink, stats = detect_tile(xys, source, queue, device=device, contexts=contexts, batch_chips=batch_chips,
                                   params=params, width=width, sink=sink, context_factory=context_factory,
-                                  upload_depth=upload_depth, tail_chips=tail_chips)
+                                  upload_depth=upload_depth, tail_chips=tail_chips, bind_numa=bind_numa)
     except Exception as e:
         if not (dist_on and dist.get_world_size() > 1):
             raise

@@ -40,6 +40,9 @@ def _declare(L):
     L.ccdgpu_init.argtypes = [c.c_int, c.POINTER(c.c_void_p)]
     L.ccdgpu_destroy.argtypes = [c.c_void_p]
     L.ccdgpu_device_count.argtypes = [c.POINTER(c.c_int)]
+    if hasattr(L, 'ccdgpu_device_numa_node'):  # (absent from libraries built before it: A/B runs)
+        L.ccdgpu_device_numa_node.argtypes = [c.c_int, c.POINTER(c.c_int)]
+        L.ccdgpu_device_numa_node.restype = c.c_int
     L.ccdgpu_synchronize.argtypes = [c.c_void_p]
     L.ccdgpu_detect_batch.argtypes = [c.c_void_p, c.POINTER(abi.Params), c.c_int32, c.c_int32,
                                       c.c_void_p, c.c_void_p, c.c_void_p, c.POINTER(abi.Result)]
@@ -82,7 +85,7 @@ EXPORTS = ('ccdgpu_version', 'ccdgpu_last_error', 'ccdgpu_params_default', 'ccdg
            'ccdgpu_run_staged', 'ccdgpu_fetch_staged', 'ccdgpu_fetch_rows', 'ccdgpu_rows_free',
            'ccdgpu_host_alloc', 'ccdgpu_host_free', 'ccdgpu_stage_slot', 'ccdgpu_run_slot',
            'ccdgpu_last_stats', 'ccdgpu_diag_counters', 'ccdgpu_stage_chips', 'ccdgpu_stage_slot_chips',
-           'ccdgpu_fetch_batch_rows')
+           'ccdgpu_fetch_batch_rows', 'ccdgpu_device_numa_node')
 
 
 def lib():
@@ -115,6 +118,13 @@ def device_count():
     n = ctypes.c_int(0)
     rc = lib().ccdgpu_device_count(ctypes.byref(n))
     return n.value if rc == 0 else 0
+
+
+def device_numa_node(device=0):
+    """NUMA node the GPU ``device`` is attached to (-1: not exposed by the platform)."""
+    n = ctypes.c_int(-1)
+    _check(lib().ccdgpu_device_numa_node(int(device), ctypes.byref(n)))
+    return n.value
 
 
 def default_params():

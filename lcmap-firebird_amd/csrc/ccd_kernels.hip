@@ -808,8 +808,36 @@ __device__ __forceinline__ int cd_sweep(Lds *L, int pc_rt, double alpha, int max
     unsigned long long dmask = bal(b >= NB);
     const unsigned long long cmask = bal(can);
     int sweeps = max_iter;
+#ifdef CCD_CD_CYCLES
+    // diagnostic: Brent cycle detection on each band group's sweep state (w, h of its 8 lanes,
+    // bitwise); det_it / det_per = sweep at which the group's state first repeated, and the period
+    long long ws = __double_as_longlong(w), hs = __double_as_longlong(h);
+    int power = 1, lam = 0, det_it = 0, det_per = 0;
+    unsigned long long cyc = 0ull;
+#endif
     for (int it = 0; it < max_iter; ++it) {
         if (dmask == ~0ull) break;
+#ifdef CCD_CD_CYCLES
+        if (it > 0) {
+            ++lam;
+            const unsigned long long eq = bal(__double_as_longlong(w) == ws && __double_as_longlong(h) == hs);
+            unsigned long long newg = 0ull;
+            for (int g = 0; g < NB; ++g)
+                if (((eq >> (8 * g)) & 0xFFull) == 0xFFull && !((cyc >> (8 * g)) & 1ull) && !((dmask >> (8 * g)) & 1ull))
+                    newg |= 0xFFull << (8 * g);
+            if ((newg >> l) & 1ull) {
+                det_it = it;
+                det_per = lam;
+            }
+            cyc |= newg;
+            if (power == lam) {
+                ws = __double_as_longlong(w);
+                hs = __double_as_longlong(h);
+                power *= 2;
+                lam = 0;
+            }
+        }
+#endif
         const unsigned long long lm = cmask & ~dmask;  // live lanes (all coordinates)
         const double w0 = w;
         cd_coord<0>(lm & COL, alpha, rgkk, gcol[0], h, w);
@@ -882,6 +910,25 @@ __device__ __forceinline__ int cd_sweep(Lds *L, int pc_rt, double alpha, int max
         }
     }
     if (b < NB && k < 7) L->coef[b][k] = act ? w : 0.0;
+#ifdef CCD_CD_CYCLES
+    {
+        // groups that ran max_iter sweeps: how many, how many of them had cycled, and the sums
+        // of their detection sweeps and periods (lane 8b stands for group b)
+        const bool mx = k == 0 && b < NB && sweeps >= max_iter;
+        const bool mc = mx && det_it > 0;
+        int v0 = mx ? 1 : 0, v1 = mc ? 1 : 0, v2 = mc ? det_it : 0, v3 = mc ? det_per : 0;
+        for (int o = 32; o > 0; o >>= 1) {
+            v0 += shfx(v0, o);
+            v1 += shfx(v1, o);
+            v2 += shfx(v2, o);
+            v3 += shfx(v3, o);
+        }
+        PH_COUNT(P, 24, v0)
+        PH_COUNT(P, 25, v1)
+        PH_COUNT(P, 26, v2)
+        PH_COUNT(P, 27, v3)
+    }
+#endif
     return sweeps;
 }
 // the sweep with its coordinate count unrolled for the three model sizes (no per-coordinate branch)
@@ -1015,10 +1062,15 @@ __device__ __forceinline__ void emit(Px &P, int sday, int eday, int bday, int co
     P.nseg++;
 }
 
-__device__ __forceinline__ void catch_(Px &P, int a, int b, int cqa) {
+// change.catch (a segment fit with the minimum coefficients over compacted [a, b)).  whole: the
+// permanent-snow / insufficient-clear procedures' single segment, which spans the input's sorted
+// dates (first to last, all observations) with break day 0.
+__device__ __forceinline__ void catch_(Px &P, int a, int b, int cqa, bool whole = false) {
     fit_models(P, a, b, ARGS().p.coef_min);
-    const int bday = b < P.m ? CDR(P, b) : CDR(P, P.m - 1);
-    emit(P, CDR(P, a), CDR(P, b - 1), bday, b - a, 0.0, cqa, 0.0);
+    const int bday = whole ? 0 : b < P.m ? CDR(P, b) : CDR(P, P.m - 1);
+    const int sday = whole ? (int)P.sd[0] : CDR(P, a);
+    const int eday = whole ? (int)P.sd[P.n - 1] : CDR(P, b - 1);
+    emit(P, sday, eday, bday, b - a, 0.0, cqa, 0.0);
 }
 
 // Bin of the 256-bin histogram L->hist2[0..255] holding the rank-th smallest entry; rank becomes
@@ -3075,10 +3127,12 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
         stat_uniform(ST_FLOPS, (unsigned long long)ne *
                 ((unsigned long long)k * (7 * 2 * 8 + 5 * 3) + (unsigned long long)nf * 6 + 5 * 48));
         PH_COUNT(P, 16, ne)
+#ifndef CCD_CD_CYCLES  // (slots 24-27 carry the coordinate-descent cycle statistics there)
         PH_COUNT(P, 24, ne <= 16 ? 1 : 0)
         PH_COUNT(P, 25, ne <= 32 ? 1 : 0)
         PH_COUNT(P, 26, nv)
         PH_COUNT(P, 27, Tm ? 0 : 1)
+#endif
         PH_END(P, cl, 7)
         const unsigned long long rem = xs >= 64 ? O : (O & ((1ull << xs) - 1ull));
         const int R = popc(rem);
@@ -3118,25 +3172,36 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
     wb = b;
 }
 
-__device__ __forceinline__ void standard_procedure(Px &P) {
+// proc: the pixel's procedure.  The permanent-snow and insufficient-clear procedures
+// (procedures.permanent_snow_procedure / insufficient_clear_procedure: one fit over every usable
+// observation when there are at least meow_size of them) run through the same catch site.
+__device__ __forceinline__ void standard_procedure(Px &P, int proc) {
     const ccdgpu_params &p = ARGS().p;
     const int meow = p.meow_size;
-    PH_BEGIN(vg)
-    variogram(P);
-    adjust_peek(P);
-    wsync();  // LDS().chg written by lane 0
-    PH_END(P, vg, 2)
     int a = 0, b = meow, prev = 0, nres = 0;
     bool start = true;
     // ccd.procedures.standard_procedure's loop with its two catch() calls (the start segment
     // before a model, the end segment after the last one) run from one site (one inlined copy of
-    // the fit): cmode 1 = the start catch, after which the iteration resumes; 2 = the end catch.
+    // the fit): cmode 1 = the start catch, after which the iteration resumes; 2 = the end catch;
+    // 3 = the whole-period segment of the other procedures.
     int cmode = 0, ca = 0, cb = 0, cq = 0;
+    if (proc != CCDGPU_PROC_STANDARD) {
+        if (P.m < meow) return;
+        cmode = 3;
+        cb = P.m;
+        cq = proc == CCDGPU_PROC_PERMANENT_SNOW ? p.curve_qa_persist_snow : p.curve_qa_insuf_clear;
+    } else {
+        PH_BEGIN(vg)
+        variogram(P);
+        adjust_peek(P);
+        wsync();  // LDS().chg written by lane 0
+        PH_END(P, vg, 2)
+    }
     for (;;) {
         bool resume = false;
         if (cmode) {
-            catch_(P, ca, cb, cq);
-            if (cmode == 2) break;
+            catch_(P, ca, cb, cq, cmode == 3);
+            if (cmode >= 2) break;
             cmode = 0;
             resume = true;
         }
@@ -3403,13 +3468,7 @@ __device__ __forceinline__ void detect_body() {
             for (int i = l; i < A.mask_words; i += W) A.mask_bits[(size_t)job * A.mask_words + i] = 0u;
             continue;
         }
-        if (proc == CCDGPU_PROC_STANDARD) {
-            standard_procedure(P);
-        } else if (P.m >= A.p.meow_size) {
-            fit_models(P, 0, P.m, A.p.coef_min);
-            emit(P, (int)P.sd[0], (int)P.sd[P.n - 1], 0, P.m, 0.0,
-                 proc == CCDGPU_PROC_PERMANENT_SNOW ? A.p.curve_qa_persist_snow : A.p.curve_qa_insuf_clear, 0.0);
-        }
+        standard_procedure(P, proc);
         wsync();
         PH_END(P, tot, 0)
         if (l == 0) {

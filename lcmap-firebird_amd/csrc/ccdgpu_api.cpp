@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cctype>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -295,6 +296,22 @@ int ccdgpu_device_count(int *count) {
         return fail(CCDGPU_EHIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
     }
     *count = c;
+    return 0;
+}
+
+int ccdgpu_device_numa_node(int device, int *node) {
+    if (!node) return fail(CCDGPU_EINVAL, "node out pointer is NULL");
+    *node = -1;
+    char bus[64] = {0};
+    HIPCHK(hipDeviceGetPCIBusId(bus, (int)sizeof(bus) - 1, device));
+    for (char *q = bus; *q; ++q) *q = (char)std::tolower((unsigned char)*q);
+    const std::string path = std::string("/sys/bus/pci/devices/") + bus + "/numa_node";
+    FILE *f = std::fopen(path.c_str(), "r");
+    if (!f) return 0;  // not exposed: unknown
+    int v = -1;
+    if (std::fscanf(f, "%d", &v) != 1) v = -1;
+    std::fclose(f);
+    *node = v;
     return 0;
 }
 

@@ -36,6 +36,16 @@ for i, n in enumerate(['batches ne<=16', 'batches ne<=32', 'batch valid lanes', 
 for i, n in enumerate(['init tmask calls', 'init fits', 'lf batched refits', 'spec calls', 'spec windows computed',
                        'spec windows installed', 'spec wave sweeps', 'spec lane sweeps']):
     out[n] = dc[8 + 32 + i]
+if os.environ.get('CCD_DIAG_LIB', '').endswith('cdcyc.so'):
+    # CCD_CD_CYCLES build: slots 24-27 = band groups that ran max_iter sweeps, those of them whose
+    # sweep state repeated (a cycle), sum of their detection sweeps, sum of their periods
+    for i, n in enumerate(['batches ne<=16', 'batches ne<=32', 'batch valid lanes', 'batches without terminal step']):
+        out.pop(n, None)
+    g, c, it, per = dc[8 + 24], dc[8 + 25], dc[8 + 26], dc[8 + 27]
+    out['cd groups at max_iter'] = g
+    out['cd groups at max_iter that cycled'] = c
+    out['mean detection sweep'] = it / c if c else None
+    out['mean period'] = per / c if c else None
 out['pixels'] = chips * 10000
 out['cycles_per_pixel'] = tot / out['pixels']
 print(json.dumps(out, indent=1))
