@@ -78,6 +78,8 @@ def parse():
     ap.add_argument('--tile-contexts', type=int, default=3, help='contexts per GPU in the tile leg')
     ap.add_argument('--tile-copy-threads', type=int, default=4, help='host threads per pool-chip copy in the tile leg source (3 contexts x 4 within the box\'s 16-CPU quota)')
     ap.add_argument('--tile-no-numa', action='store_true', help='tile leg: leave host threads unbound (A/B)')
+    ap.add_argument('--tile-no-encode', action='store_true',
+                    help='tile leg: upload raw chips (pool copies into pinned batches) instead of the lossless transport encoding (A/B)')
     ap.add_argument('--tile-depth', type=int, default=2, help='batches each tile-leg context keeps uploaded ahead')
     ap.add_argument('--share-device', action='store_true',
                     help='rehearsal only: ranks beyond the device count share devices (LOCAL_RANK mod count)')
@@ -209,10 +211,11 @@ def main():
             'scaling': 'weak',
             'vs_baseline': None,
             'dtype': 'f64',
-            'data': 'synthetic (Landsat 4-8 ARD, seeded; tile leg: every chip distinct, generated on the GPU into pinned host memory)',
+            'data': 'synthetic (Landsat 4-8 ARD, seeded; tile leg: every chip distinct -- date-shifted copies of GPU-generated pool chips)',
             'config': {
                 'workload': '%s; one full 5000x5000-pixel tile per GPU (%d distinct 100x100-pixel chips per rank, %s), '
-                            'PCIe-inclusive: chips uploaded from pinned host memory, detected, segment/pixel rows packed '
+                            'PCIe-inclusive: chips uploaded from pinned host memory (lossless transport encoding unless '
+                            '--tile-no-encode), detected, segment/pixel rows packed '
                             'on the device and fetched back, per-chip summaries gathered on rank 0 (ccdc.runner.changedetection); '
                             'a step = %d chips per rank' % (
                                 CONFIG_NAMES[args.config], tl['chips_per_rank'],
@@ -375,6 +378,13 @@ class _Offset(object):
     def __call__(self, positions):
         return self.src([p + self.off for p in positions])
 
+    @property
+    def has_views(self):
+        return getattr(self.src, 'has_views', hasattr(self.src, 'views'))
+
+    def views(self, positions):
+        return self.src.views([p + self.off for p in positions])
+
     def release(self, batch):
         self.src.release(batch)
 
@@ -425,9 +435,18 @@ def tile_leg(args, cfg, rank, world, device, dist):
     t_prep = time.perf_counter()
     src.prepare()
     # pinned batches in flight per context: depth + 1 (fetched or staged; the runner's slot permits)
-    src.prefill(args.tile_contexts * (args.tile_depth + 1) + 1)
+    n_inflight = args.tile_contexts * (args.tile_depth + 1) + 1
+    encode = not args.tile_no_encode
+    if encode:
+        # the runner's transport encoding (ccdc.runner.EncodingSource): each batch is encoded from
+        # the pool chips' own arrays into pinned buffers by the fetch thread and decoded on the GPU
+        esrc = runner.EncodingSource(src, threads=args.tile_copy_threads)
+        esrc.prefill(n_inflight, B, 10000, src.max_obs)
+        src_timed = src_warm = esrc
+    else:
+        src.prefill(n_inflight)
+        src_timed = src_warm = src
     prep_s = time.perf_counter() - t_prep
-    src_timed = src_warm = src
     ctxs = [ccdgpu.Context(device) for _ in range(args.tile_contexts)]
     lent = iter([])
 
@@ -443,23 +462,32 @@ def tile_leg(args, cfg, rank, world, device, dist):
         lent = iter(ctxs)
         sink = runner.SummarySink(digest=False)
         xys = [xy(p) for p in range(n)]
+        # (encode=False: the source is already the encoding wrapper when the leg encodes)
         return runner.changedetection(xys, src, device=device, contexts=args.tile_contexts, batch_chips=B,
                                       sink=sink, upload_depth=args.tile_depth, context_factory=factory,
-                                      bind_numa=not args.tile_no_numa)
+                                      bind_numa=not args.tile_no_numa, encode=False)
 
     if warm_total:
         run(warm_total, _Offset(src_warm, 1000000))
     if dist is not None:
         dist.barrier()
     ctxs[0].synchronize()
-    gen0 = src_timed.generate_seconds
+    gen0 = src.generate_seconds
+    enc0 = (esrc.bytes_raw, esrc.bytes_sent, esrc.encode_seconds) if encode else (0, 0, 0.0)
     t = time.perf_counter()
     res = run(total, src_timed)
     ctxs[0].synchronize()
     if dist is not None:
         dist.barrier()
     el = max_over_ranks(time.perf_counter() - t, dist)
-    gen_s = src_timed.generate_seconds - gen0
+    gen_s = src.generate_seconds - gen0
+    enc_stats = None
+    if encode:
+        raw_b, sent_b = esrc.bytes_raw - enc0[0], esrc.bytes_sent - enc0[1]
+        enc_stats = {'upload_bytes_raw_rank0': raw_b, 'upload_bytes_sent_rank0': sent_b,
+                     'sent_over_raw': round(sent_b / raw_b, 4) if raw_b else None,
+                     'encode_thread_seconds_rank0': round(esrc.encode_seconds - enc0[2], 3),
+                     'encoder_avx512_vbmi2': bool(ccdgpu.encode_vector_path())}
     for c in ctxs:
         c.close()
     src.close()
@@ -480,15 +508,19 @@ def tile_leg(args, cfg, rank, world, device, dist):
             'source_mode': mode, 'source_pool_chips': args.tile_pool if mode == 'pool' else None,
             'source_copy_threads': args.tile_copy_threads if mode == 'pool' else None,
             'gpu_numa_node': numa_node, 'host_threads_bound_to_gpu_node': not args.tile_no_numa,
+            'transport_encoding': enc_stats,
             'source_prepare_seconds': round(prep_s, 2),
             'generate_seconds_rank0': round(gen_s, 3),
-            'pinned_pool_batches': src_timed.allocated,
+            'pinned_pool_batches': src.allocated,
             'worker_seconds_rank0': {k: round(v, 3) for k, v in ranks[0].items() if k.endswith('_seconds')},
             'note': 'ccdc.runner tile driver over distinct chip inputs (pool mode: %d GPU-generated chips generated before '
                     'the timed run, each tile position a copy of one of its cadence with the acquisition dates moved by a '
-                    'position-dependent multiple of 16 days, copied into pinned batches by the runner\'s fetch threads; '
-                    'generate mode: every chip generated on the GPU into pinned host memory): H2D upload overlapped with '
-                    'detection, device row packing, D2H of rows, gather of per-chip summaries on rank 0' % args.tile_pool}
+                    'position-dependent multiple of 16 days; generate mode: every chip generated on the GPU into pinned '
+                    'host memory); %s; H2D upload overlapped with detection, device row packing, D2H of rows, gather of '
+                    'per-chip summaries on rank 0' % (args.tile_pool,
+                    'each batch losslessly transport-encoded by the runner\'s fetch threads straight from the chip '
+                    'arrays into pinned buffers (fill bands dropped, QA as palette codes) and decoded on the GPU'
+                    if encode else 'chips copied into pinned batches by the runner\'s fetch threads, uploaded raw')}
 
 
 def synth_nobs(cfg, c):

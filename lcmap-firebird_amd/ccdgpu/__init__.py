@@ -40,6 +40,16 @@ def _declare(L):
     L.ccdgpu_init.argtypes = [c.c_int, c.POINTER(c.c_void_p)]
     L.ccdgpu_destroy.argtypes = [c.c_void_p]
     L.ccdgpu_device_count.argtypes = [c.POINTER(c.c_int)]
+    if hasattr(L, 'ccdgpu_encode_chips'):  # (absent from libraries built before it: A/B runs)
+        L.ccdgpu_encoded_bound.argtypes = [c.c_int32, c.c_void_p, c.c_void_p]
+        L.ccdgpu_encoded_bound.restype = c.c_int64
+        L.ccdgpu_encode_chips.argtypes = [c.c_int32, c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p,
+                                          c.c_int64, c.c_int32]
+        L.ccdgpu_encode_chips.restype = c.c_int64
+        L.ccdgpu_encode_vector_path.restype = c.c_int32
+        L.ccdgpu_stage_slot_encoded.argtypes = [c.c_void_p, c.c_int32, c.c_void_p, c.c_int32, c.c_void_p, c.c_void_p,
+                                                c.c_void_p, c.c_void_p, c.c_int64]
+        L.ccdgpu_stage_slot_encoded.restype = c.c_int
     if hasattr(L, 'ccdgpu_device_numa_node'):  # (absent from libraries built before it: A/B runs)
         L.ccdgpu_device_numa_node.argtypes = [c.c_int, c.POINTER(c.c_int)]
         L.ccdgpu_device_numa_node.restype = c.c_int
@@ -85,7 +95,8 @@ EXPORTS = ('ccdgpu_version', 'ccdgpu_last_error', 'ccdgpu_params_default', 'ccdg
            'ccdgpu_run_staged', 'ccdgpu_fetch_staged', 'ccdgpu_fetch_rows', 'ccdgpu_rows_free',
            'ccdgpu_host_alloc', 'ccdgpu_host_free', 'ccdgpu_stage_slot', 'ccdgpu_run_slot',
            'ccdgpu_last_stats', 'ccdgpu_diag_counters', 'ccdgpu_stage_chips', 'ccdgpu_stage_slot_chips',
-           'ccdgpu_fetch_batch_rows', 'ccdgpu_device_numa_node')
+           'ccdgpu_fetch_batch_rows', 'ccdgpu_device_numa_node', 'ccdgpu_encoded_bound', 'ccdgpu_encode_chips',
+           'ccdgpu_encode_vector_path', 'ccdgpu_stage_slot_encoded')
 
 
 def lib():
@@ -210,6 +221,107 @@ class ChipBatch(object):
         return bits[int(self.pix_off[c]):int(self.pix_off[c + 1]), :(int(self.n_obs[c]) + 31) // 32]
 
 
+class EncodedBatch(ChipBatch):
+    """A batch in the transport encoding of ccdgpu_encode_chips (include/ccdgpu.h): the chips'
+    dates plus one byte buffer, uploaded with Context.stage_slot_encoded and decoded on the device
+    into the ChipBatch layout.  Shape, dates and mask helpers as ChipBatch; chip(c) gives
+    (dates, None, None) -- the pixel data exist only in encoded form.
+
+        e = EncodedBatch.encode([(d0, s0, q0), (d1, s1, q1)], storage=encode_storage(...))
+    """
+
+    def __init__(self, n_pix, n_obs, storage=None, pinned=True):
+        self.n_pix = np.ascontiguousarray(n_pix, dtype=np.int32).reshape(-1)
+        self.n_obs = np.ascontiguousarray(n_obs, dtype=np.int32).reshape(-1)
+        if self.n_pix.shape != self.n_obs.shape or self.n_pix.size == 0:
+            raise ValueError('n_pix and n_obs must be equal-length, non-empty')
+        self.obs_off = np.concatenate([[0], np.cumsum(self.n_obs, dtype=np.int64)])
+        self.pix_off = np.concatenate([[0], np.cumsum(self.n_pix, dtype=np.int64)])
+        self.data_off = np.concatenate([[0], np.cumsum(self.n_pix.astype(np.int64) * self.n_obs)])
+        bound = int(lib().ccdgpu_encoded_bound(self.n_chips, self.n_pix.ctypes.data, self.n_obs.ctypes.data))
+        nd = int(self.obs_off[-1])
+        self.storage = storage
+        if storage is not None:
+            sd, sb = storage
+            if sd.dtype != np.int64 or sb.dtype != np.uint8 or sd.size < nd or sb.size < bound:
+                raise ValueError('storage too small or of the wrong types for this batch')
+            self.dates, self.buf = sd[:nd], sb
+        else:
+            alloc = pinned_empty if pinned else np.empty
+            self.dates, self.buf = alloc((nd,), np.int64), alloc((bound,), np.uint8)
+        self.spectra = self.qa = None
+        self.bound = bound
+        self.nbytes_encoded = 0
+
+    @property
+    def nbytes(self):
+        return self.dates.nbytes + self.nbytes_encoded
+
+    def chip(self, c):
+        n, o = int(self.n_obs[c]), int(self.obs_off[c])
+        return self.dates[o:o + n], None, None
+
+    def set_chip(self, c, dates, spectra, qa):
+        raise TypeError('EncodedBatch holds encoded chips: build it with EncodedBatch.encode')
+
+    def fill(self, chips, threads=4):
+        """Encode chips [(dates [n], spectra [7][n_pix][n] int16, qa [n_pix][n] uint16), ...]
+        (any C-contiguous arrays: pinned batch views, or a source's own arrays -- nothing else is
+        copied) into this batch; returns the encoded bytes."""
+        chips = list(chips)
+        if len(chips) != self.n_chips:
+            raise ValueError('%d chips for a batch of %d' % (len(chips), self.n_chips))
+        sp = (ctypes.c_void_p * len(chips))()
+        qp = (ctypes.c_void_p * len(chips))()
+        keep = []
+        for i, (d, s, q) in enumerate(chips):
+            d = np.asarray(d)
+            s = np.ascontiguousarray(s, dtype=np.int16)
+            q = np.ascontiguousarray(q, dtype=np.uint16)
+            if d.shape != (int(self.n_obs[i]),) or s.shape != (7, int(self.n_pix[i]), int(self.n_obs[i])) or \
+                    q.shape != (int(self.n_pix[i]), int(self.n_obs[i])):
+                raise ValueError('chip %d does not have this batch\'s shape' % i)
+            o = int(self.obs_off[i])
+            self.dates[o:o + d.shape[0]] = d
+            sp[i], qp[i] = s.ctypes.data, q.ctypes.data
+            keep.append((s, q))
+        n = int(lib().ccdgpu_encode_chips(self.n_chips, self.n_pix.ctypes.data, self.n_obs.ctypes.data,
+                                          ctypes.cast(sp, ctypes.c_void_p), ctypes.cast(qp, ctypes.c_void_p),
+                                          self.buf.ctypes.data, self.buf.size, int(threads)))
+        if n < 0:
+            raise ValueError('ccdgpu_encode_chips failed (%d)' % n)
+        self.nbytes_encoded = n
+        return n
+
+    @classmethod
+    def encode(cls, chips, threads=4, storage=None, pinned=True):
+        chips = list(chips)
+        b = cls([c[2].shape[0] for c in chips], [c[0].shape[0] for c in chips], storage=storage, pinned=pinned)
+        b.fill(chips, threads)
+        return b
+
+    def chip_modes(self):
+        """Per chip: 1 if encoded, 0 if sent raw (from the section headers)."""
+        off = self.buf[8:8 * (self.n_chips + 2)].view(np.int64)
+        return [int(self.buf[int(o):int(o) + 4].view(np.int32)[0]) for o in off[:self.n_chips]]
+
+
+def encode_storage(max_chips, max_pix, max_obs, pinned=True):
+    """Reusable buffers for EncodedBatch(..., storage=...): room for ``max_chips`` chips of up to
+    ``max_pix`` pixels x ``max_obs`` observations."""
+    n = int(max_chips)
+    np_ = np.full(n, int(max_pix), dtype=np.int32)
+    no = np.full(n, int(max_obs), dtype=np.int32)
+    bound = int(lib().ccdgpu_encoded_bound(n, np_.ctypes.data, no.ctypes.data))
+    alloc = pinned_empty if pinned else np.empty
+    return alloc((n * int(max_obs),), np.int64), alloc((bound,), np.uint8)
+
+
+def encode_vector_path():
+    """True if the encoder uses AVX-512 VBMI2 compress-stores on this CPU."""
+    return bool(lib().ccdgpu_encode_vector_path())
+
+
 def _as_inputs(dates, spectra, qa):
     dates = np.ascontiguousarray(dates, dtype=np.int64)
     spectra = np.ascontiguousarray(spectra, dtype=np.int16)
@@ -290,12 +402,26 @@ class Context(object):
     def stage_slot_chips(self, slot, batch, params=None):
         """Upload a ChipBatch into input slot 0 .. UPLOAD_SLOTS-1 on the copy stream and return at once (the
         batch must stay alive and unchanged until run_slot(slot) returns; pinned=True batches
-        upload asynchronously)."""
+        upload asynchronously).  An EncodedBatch goes through stage_slot_encoded."""
+        if isinstance(batch, EncodedBatch):
+            return self.stage_slot_encoded(slot, batch, params)
         p = params if isinstance(params, abi.Params) else abi.params_from_dict(params)
         _check(lib().ccdgpu_stage_slot_chips(self._ctx, int(slot), ctypes.byref(p), batch.n_chips,
                                              batch.n_pix.ctypes.data, batch.n_obs.ctypes.data,
                                              batch.dates.ctypes.data, batch.spectra.ctypes.data,
                                              batch.qa.ctypes.data))
+        if not hasattr(self, '_slot_keep'):
+            self._slot_keep = {}
+        self._slot_keep[int(slot)] = batch
+
+    def stage_slot_encoded(self, slot, batch, params=None):
+        """Upload an EncodedBatch into input slot ``slot`` and decode it there on the device (copy
+        stream; same life-time rules as stage_slot_chips)."""
+        p = params if isinstance(params, abi.Params) else abi.params_from_dict(params)
+        _check(lib().ccdgpu_stage_slot_encoded(self._ctx, int(slot), ctypes.byref(p), batch.n_chips,
+                                               batch.n_pix.ctypes.data, batch.n_obs.ctypes.data,
+                                               batch.dates.ctypes.data, batch.buf.ctypes.data,
+                                               int(batch.nbytes_encoded)))
         if not hasattr(self, '_slot_keep'):
             self._slot_keep = {}
         self._slot_keep[int(slot)] = batch
@@ -371,9 +497,10 @@ class Context(object):
     def staged_inputs(self):
         """The staged pixel inputs copied back: (spectra [C][7][n_pix][n], qa [C][n_pix][n]) for
         a uniform batch, flat (spectra, qa) in the ChipBatch layout for a stage_chips batch."""
-        if isinstance(self._keep, ChipBatch):
+        if isinstance(self._keep, ChipBatch):  # (an EncodedBatch too: decoded on the device)
             b = self._keep
-            spectra, qa = np.empty_like(np.asarray(b.spectra)), np.empty_like(np.asarray(b.qa))
+            nd = int(b.data_off[-1])
+            spectra, qa = np.empty(7 * nd, dtype=np.int16), np.empty(nd, dtype=np.uint16)
             _check(lib().ccdgpu_staged_inputs(self._ctx, spectra.ctypes.data, qa.ctypes.data))
             return spectra, qa
         d = self._keep[0]

@@ -257,6 +257,31 @@ class TileSource(object):
             self.generate_seconds += time.perf_counter() - t
         return b
 
+    @property
+    def has_views(self):
+        return self.mode == 'pool'
+
+    def views(self, positions):
+        """'pool' mode without the copy: per position (dates, spectra, qa) where the dates are
+        the position's own (moved) acquisition dates and spectra / qa are the pool chip's arrays
+        themselves -- for a consumer that makes its own pass over them (ccdc.runner's
+        EncodingSource encodes straight from them into pinned memory)."""
+        if self.mode != 'pool':
+            raise AttributeError('views exist in pool mode only')
+        if self._pool is None:
+            raise RuntimeError("TileSource('pool'): call prepare() first")
+        import time
+        t = time.perf_counter()
+        out = []
+        for p in positions:
+            c = self.chip_of(p)
+            d = self._dates(c)
+            (_, pd, ps, pq), days = self._pool_chip(p, c, d)
+            out.append((pd + days, ps, pq))
+        with self._lock:
+            self.generate_seconds += time.perf_counter() - t
+        return out
+
     def _dates(self, c):
         key = int(c)
         cache = getattr(self, '_date_cache', None)

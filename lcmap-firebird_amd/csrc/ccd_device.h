@@ -93,6 +93,8 @@ int ccdk_occupancy(int variant, int32_t n_obs);
 int ccdk_unpack_b64(const unsigned char *text, int64_t text_bytes, const int64_t *offsets, int32_t n_chips,
                     int32_t n_obs, int32_t n_pix, int16_t *spectra, uint16_t *qa, unsigned long long *err,
                     void *stream);
+// transport-encoded batch (ccd_encode.c) -> spectra / qa in the standard layout (ccd_pack.hip)
+int ccdk_decode_enc(const unsigned char *enc, int64_t total_pix, int16_t *spectra, uint16_t *qa, void *stream);
 // detection results -> segment / pixel table rows (ccd_rows.hip)
 int ccdk_pack_rows(const ccdgpu_segment *seg, const int64_t *seg_off, const int64_t *row_off, const uint32_t *mask_bits,
                    int32_t mask_words, int32_t n_pix, int32_t n_obs, int32_t cx, int32_t cy, int32_t width,

@@ -1,0 +1,331 @@
+/* ccd_encode.c -- lossless transport encoding of ARD chips for the PCIe upload (host side).
+ *
+ * The tile path is bound by the host-to-device link (16 bytes per observation: 7 int16 bands +
+ * a uint16 QA word).  Two properties of Landsat ARD make those bytes compressible
+ * without loss, and both are checked per chip, so the encoding is exact for any input:
+ *   - a fill observation (pixel_qa bit 0, qa.py's fill bit) carries the ARD fill value -9999 in
+ *     every band: its band values are dropped and restored on the device;
+ *   - a chip's QA words take a handful of distinct values: each becomes a 4-bit index into a
+ *     16-entry palette.
+ * A chip with a fill observation whose bands are not all -9999, or with more than 16 distinct QA
+ * words, is sent raw (mode 0).  The device decoder (ccd_decode_enc in ccd_pack.hip) rebuilds the
+ * standard band-major [7][n_pix][n_obs] spectra and [n_pix][n_obs] QA of every chip bit for bit,
+ * so detection runs unchanged (tests/test_encode.py: round trips against a numpy decoder;
+ * tests/test_gpu_encode.py: device decode == raw upload).  Layout: include/ccdgpu.h.
+ *
+ * The encode replaces the copy into pinned memory that every upload from a fetched (pageable)
+ * chip needs anyway; it runs one pass over the QA words (counts, palette, fill check) and one
+ * over the bands (stream compaction: AVX-512 VBMI2 compress-store where the CPU has it).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "ccdgpu.h"
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define ENC_HDR 128
+#define ENC_ALIGN 256
+
+static size_t up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+/* bytes of a chip section in mode 1 for kept observations, and in mode 0 */
+static size_t sec_mode1(int64_t n_pix, int64_t n_obs, int64_t kept) {
+    return ENC_HDR + up(4 * (size_t)(n_pix + 1), 16) + up((size_t)n_pix * (size_t)((n_obs + 1) / 2), 16) +
+           7 * 2 * up((size_t)kept, 8);
+}
+static size_t sec_mode0(int64_t n_pix, int64_t n_obs) {
+    const size_t d = (size_t)n_pix * (size_t)n_obs;
+    return ENC_HDR + up(2 * d, 16) + 7 * 2 * d;
+}
+static size_t table_bytes(int32_t n_chips) { return up(8 + 16 * ((size_t)n_chips + 1), ENC_ALIGN); }
+
+int64_t ccdgpu_encoded_bound(int32_t n_chips, const int32_t *n_pix, const int32_t *n_obs) {
+    if (n_chips <= 0 || !n_pix || !n_obs) return -1;
+    size_t t = table_bytes(n_chips);
+    for (int32_t c = 0; c < n_chips; ++c) {
+        const size_t a = sec_mode0(n_pix[c], n_obs[c]), b = sec_mode1(n_pix[c], n_obs[c], (int64_t)n_pix[c] * n_obs[c]);
+        t += up(a > b ? a : b, ENC_ALIGN);
+    }
+    return (int64_t)t;
+}
+
+/* ---- band compaction: dst[k++] = src[i] for the observations kept (keep[i] = 1); *bad is set
+ * when a dropped (fill) observation's value is not -9999 (the chip then goes raw) */
+static size_t compact_scalar(const int16_t *src, const uint8_t *keep, int n, int16_t *dst, int *bad) {
+    size_t k = 0;
+    int b = 0;
+    for (int i = 0; i < n; ++i) {
+        dst[k] = src[i];
+        k += keep[i];
+        b |= !keep[i] & (src[i] != -9999);
+    }
+    *bad |= b;
+    return k;
+}
+
+#if defined(__x86_64__)
+#include <immintrin.h>
+/* the same with AVX-512 VBMI2, 32 observations at a time; m[] = keep bit masks.  The kept values
+ * are compressed in a register and written with a masked store of exactly their count (a
+ * compress with a memory destination is microcoded and slow on Zen 4/5). */
+__attribute__((target("avx512f,avx512bw,avx512vbmi2"))) static size_t compact_vbmi2(const int16_t *src,
+                                                                                   const uint32_t *m, int n,
+                                                                                   int16_t *dst, int *bad) {
+    size_t k = 0;
+    int i = 0, w = 0;
+    const __m512i fillv = _mm512_set1_epi16(-9999);
+    __mmask32 nb = 0;  /* dropped observations whose value is not the fill value */
+    for (; i + 32 <= n; i += 32, ++w) {
+        const __m512i v = _mm512_loadu_si512((const void *)(src + i));
+        const int c = __builtin_popcount(m[w]);
+        _mm512_mask_storeu_epi16(dst + k, (__mmask32)(c == 32 ? 0xFFFFFFFFu : (1u << c) - 1u),
+                                 _mm512_maskz_compress_epi16((__mmask32)m[w], v));
+        k += (size_t)c;
+        nb |= _mm512_mask_cmpneq_epi16_mask((__mmask32)~m[w], v, fillv);
+    }
+    if (i < n) {
+        const __mmask32 tail = (__mmask32)((1ull << (n - i)) - 1ull);
+        const __m512i v = _mm512_maskz_loadu_epi16(tail, (const void *)(src + i));
+        const int c = __builtin_popcount(m[w] & tail);
+        _mm512_mask_storeu_epi16(dst + k, (__mmask32)((1u << c) - 1u), _mm512_maskz_compress_epi16((__mmask32)(m[w] & tail), v));
+        k += (size_t)c;
+        nb |= _mm512_mask_cmpneq_epi16_mask((__mmask32)(~m[w] & tail), v, fillv);
+    }
+    *bad |= nb != 0;
+    return k;
+}
+/* 4-bit palette codes (two per byte, even observation in the low nibble) and the keep bit masks
+ * of one pixel's QA row, 32 observations at a time: a code is the index of the palette entry its
+ * word equals (at most 16 compares); the codes' 16-bit lanes, read as 32-bit pairs, fold into
+ * bytes with one down-convert. */
+__attribute__((target("avx512f,avx512bw,avx512vl,avx512vbmi2"))) static void qa_codes_avx512(const uint16_t *q, int n,
+                                                                                   const uint16_t *pal, int npal,
+                                                                                   uint8_t *r, uint32_t *km) {
+    int i = 0, w = 0;
+    const __m512i one = _mm512_set1_epi16(1);
+    for (; i < n; i += 32, ++w) {
+        const __mmask32 lm = n - i >= 32 ? (__mmask32)0xFFFFFFFFu : (__mmask32)((1u << (n - i)) - 1u);
+        const __m512i v = _mm512_maskz_loadu_epi16(lm, (const void *)(q + i));
+        __m512i code = _mm512_setzero_si512();
+        for (int j = 1; j < npal; ++j)
+            code = _mm512_mask_mov_epi16(code, _mm512_cmpeq_epi16_mask(v, _mm512_set1_epi16((short)pal[j])),
+                                         _mm512_set1_epi16((short)j));
+        km[w] = (uint32_t)(_mm512_testn_epi16_mask(v, one) & lm);
+        const __m512i pr = _mm512_or_si512(_mm512_and_si512(code, _mm512_set1_epi32(0xF)),
+                                           _mm512_and_si512(_mm512_srli_epi32(code, 12), _mm512_set1_epi32(0xF0)));
+        const __m128i bytes = _mm512_cvtepi32_epi8(pr);
+        const int nb = (n - i >= 32 ? 32 : n - i + 1) / 2;  /* bytes of this chunk's codes */
+        _mm_mask_storeu_epi8(r + (i >> 1), (__mmask16)(nb == 16 ? 0xFFFFu : (1u << nb) - 1u), bytes);
+    }
+}
+static int have_vbmi2(void) {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("CCDGPU_ENCODE_SCALAR");
+        v = (e && *e && *e != '0') ? 0 : __builtin_cpu_supports("avx512vbmi2") && __builtin_cpu_supports("avx512bw") &&
+                                                  __builtin_cpu_supports("avx512vl");
+    }
+    return v;
+}
+#else
+static int have_vbmi2(void) { return 0; }
+#endif
+
+int32_t ccdgpu_encode_vector_path(void) { return have_vbmi2(); }
+
+/* per-thread pass-1 state: the QA words seen (a 65536-bit set), a fill observation with a band
+ * value other than -9999 */
+typedef struct {
+    uint8_t seen[65536];  /* (byte flags: independent stores, no read-modify-write chain) */
+    int bad_fill;
+} pass1_t;
+
+/* mode 0: the chip as it is (header fields other than the mode already written) */
+static size_t encode_raw(int32_t n_pix, int32_t n_obs, const int16_t *spectra, const uint16_t *qa, uint8_t *sec,
+                         int nt) {
+    const size_t plane = (size_t)n_pix * (size_t)n_obs;
+    int32_t *h = (int32_t *)sec;
+    h[0] = 0;
+    h[3] = 0;
+    int64_t *h64 = (int64_t *)(sec + 48);
+    h64[0] = 0;
+    h64[2] = 0;
+    memset(sec + 16, 0, 32);
+    uint16_t *oq = (uint16_t *)(sec + ENC_HDR);
+    int16_t *os = (int16_t *)(sec + ENC_HDR + up(2 * plane, 16));
+#pragma omp parallel for schedule(static) num_threads(nt)
+    for (int32_t p = 0; p < n_pix; ++p) {
+        memcpy(oq + (size_t)p * n_obs, qa + (size_t)p * n_obs, 2 * (size_t)n_obs);
+        for (int b = 0; b < 7; ++b)
+            memcpy(os + (size_t)b * plane + (size_t)p * n_obs, spectra + (size_t)b * plane + (size_t)p * n_obs,
+                   2 * (size_t)n_obs);
+    }
+    return sec_mode0(n_pix, n_obs);
+}
+
+/* one chip into sec (room for the larger of its two modes); returns the section's bytes */
+static size_t encode_chip(int32_t n_pix, int32_t n_obs, const int16_t *spectra, const uint16_t *qa, int64_t pix_base,
+                          int64_t data_off, uint8_t *sec, int threads, uint32_t *kept_scratch) {
+    const size_t plane = (size_t)n_pix * (size_t)n_obs;
+    int nt = threads > 0 ? threads : 1;
+    if (nt > 64) nt = 64;
+    pass1_t *st = (pass1_t *)calloc((size_t)nt, sizeof(pass1_t));
+    uint8_t *lut = (uint8_t *)malloc(65536);  /* QA word -> palette index */
+    if (!st || !lut) {
+        free(st);
+        free(lut);
+        return 0;
+    }
+    /* pass 1: kept counts, distinct QA words, fill observations' band values */
+#pragma omp parallel for schedule(static) num_threads(nt)
+    for (int32_t p = 0; p < n_pix; ++p) {
+#ifdef _OPENMP
+        pass1_t *s = &st[omp_get_thread_num()];
+#else
+        pass1_t *s = &st[0];
+#endif
+        const uint16_t *q = qa + (size_t)p * n_obs;
+        uint32_t fill = 0;
+        for (int32_t i = 0; i < n_obs; ++i) {
+            const uint16_t v = q[i];
+            s->seen[v] = 1;
+            fill += v & 1u;
+        }
+        kept_scratch[p] = (uint32_t)n_obs - fill;
+    }
+    int bad = 0;  /* (pass 2 checks the fill observations' band values) */
+    uint16_t palv[16];
+    int npal = 0;
+    for (int t = 0; t < nt; ++t) bad |= st[t].bad_fill;
+    {
+        uint64_t *s0 = (uint64_t *)st[0].seen;
+        for (int t = 1; t < nt; ++t) {
+            const uint64_t *st_ = (const uint64_t *)st[t].seen;
+            for (int w = 0; w < 8192; ++w) s0[w] |= st_[w];
+        }
+        for (int w = 0; w < 8192 && npal <= 16; ++w)  /* ascending: the palette is sorted */
+            if (s0[w])
+                for (int j = 0; j < 8 && npal <= 16; ++j)
+                    if (st[0].seen[8 * w + j]) {
+                        if (npal < 16) palv[npal] = (uint16_t)(8 * w + j);
+                        ++npal;
+                    }
+    }
+    free(st);
+    int32_t *h = (int32_t *)sec;
+    memset(sec, 0, ENC_HDR);
+    h[1] = n_pix;
+    h[2] = n_obs;
+    int64_t *h64 = (int64_t *)(sec + 48);
+    h64[1] = data_off;
+    h64[3] = pix_base;
+    if (bad || npal > 16) {
+        free(lut);
+        return encode_raw(n_pix, n_obs, spectra, qa, sec, nt);
+    }
+    h[0] = 1;
+    h[3] = npal;
+    uint16_t *pal = (uint16_t *)(sec + 16);
+    for (int j = 0; j < npal; ++j) {
+        pal[j] = palv[j];
+        lut[palv[j]] = (uint8_t)j;
+    }
+    uint32_t *koff = (uint32_t *)(sec + ENC_HDR);
+    uint64_t tot = 0;
+    for (int32_t p = 0; p < n_pix; ++p) {
+        koff[p] = (uint32_t)tot;
+        tot += kept_scratch[p];
+    }
+    koff[n_pix] = (uint32_t)tot;
+    const size_t bstride = up((size_t)tot, 8);
+    h64[0] = (int64_t)tot;
+    h64[2] = (int64_t)bstride;
+    uint8_t *q4 = sec + ENC_HDR + up(4 * ((size_t)n_pix + 1), 16);
+    const size_t rowb = (size_t)(n_obs + 1) / 2;
+    int16_t *bands = (int16_t *)(q4 + up((size_t)n_pix * rowb, 16));
+    const int vec = have_vbmi2();
+    int bad2 = 0;
+    /* pass 2: 4-bit QA codes and the kept band values (and the fill observations' values checked) */
+#pragma omp parallel num_threads(nt) reduction(| : bad2)
+    {
+        uint8_t *keep = (uint8_t *)malloc((size_t)n_obs + 64);
+        uint32_t *km = (uint32_t *)malloc(((size_t)n_obs / 32 + 2) * 4);
+#pragma omp for schedule(static)
+        for (int32_t p = 0; p < n_pix; ++p) {
+            const uint16_t *q = qa + (size_t)p * n_obs;
+            uint8_t *r = q4 + (size_t)p * rowb;
+#if defined(__x86_64__)
+            if (vec) {
+                qa_codes_avx512(q, n_obs, pal, npal, r, km);
+                for (int b = 0; b < 7; ++b)
+                    compact_vbmi2(spectra + (size_t)b * plane + (size_t)p * n_obs, km, n_obs,
+                                  bands + (size_t)b * bstride + koff[p], &bad2);
+                continue;
+            }
+#endif
+            memset(km, 0, ((size_t)n_obs / 32 + 1) * 4);
+            int32_t i = 0;
+            for (; i + 1 < n_obs; i += 2) {
+                const uint16_t v0 = q[i], v1 = q[i + 1];
+                r[i >> 1] = (uint8_t)(lut[v0] | (lut[v1] << 4));
+                const uint32_t k0 = !(v0 & 1u), k1 = !(v1 & 1u);
+                keep[i] = (uint8_t)k0;
+                keep[i + 1] = (uint8_t)k1;
+                km[i >> 5] |= (k0 | (k1 << 1)) << (i & 31);
+            }
+            if (i < n_obs) {
+                const uint16_t v0 = q[i];
+                r[i >> 1] = lut[v0];
+                const uint32_t k0 = !(v0 & 1u);
+                keep[i] = (uint8_t)k0;
+                km[i >> 5] |= k0 << (i & 31);
+            }
+            for (int b = 0; b < 7; ++b)
+                compact_scalar(spectra + (size_t)b * plane + (size_t)p * n_obs, keep, n_obs,
+                               bands + (size_t)b * bstride + koff[p], &bad2);
+        }
+        free(keep);
+        free(km);
+    }
+    free(lut);
+    if (bad2) return encode_raw(n_pix, n_obs, spectra, qa, sec, nt);  /* a fill observation with data */
+    return sec_mode1(n_pix, n_obs, (int64_t)tot);
+}
+
+int64_t ccdgpu_encode_chips(int32_t n_chips, const int32_t *n_pix, const int32_t *n_obs, const int16_t *const *spectra,
+                            const uint16_t *const *qa, uint8_t *out, int64_t out_cap, int32_t threads) {
+    if (n_chips <= 0 || !n_pix || !n_obs || !spectra || !qa || !out) return -1;
+    const int64_t need = ccdgpu_encoded_bound(n_chips, n_pix, n_obs);
+    if (need < 0 || out_cap < need) return -2;
+    int64_t *tab = (int64_t *)out;
+    tab[0] = n_chips;
+    int64_t *off = tab + 1, *pix = tab + 2 + n_chips;
+    int32_t maxp = 0;
+    for (int32_t c = 0; c < n_chips; ++c) {
+        if (n_pix[c] <= 0 || n_obs[c] <= 0 || !spectra[c] || !qa[c]) return -1;
+        maxp = n_pix[c] > maxp ? n_pix[c] : maxp;
+    }
+    uint32_t *kept = (uint32_t *)malloc(4 * (size_t)maxp);
+    if (!kept) return -3;
+    size_t pos = table_bytes(n_chips);
+    int64_t pbase = 0, dbase = 0;
+    for (int32_t c = 0; c < n_chips; ++c) {
+        off[c] = (int64_t)pos;
+        pix[c] = pbase;
+        const size_t sz = encode_chip(n_pix[c], n_obs[c], spectra[c], qa[c], pbase, dbase, out + pos, threads, kept);
+        if (!sz) {
+            free(kept);
+            return -3;
+        }
+        pos += up(sz, ENC_ALIGN);
+        pbase += n_pix[c];
+        dbase += (int64_t)n_pix[c] * n_obs[c];
+    }
+    off[n_chips] = (int64_t)pos;
+    pix[n_chips] = pbase;
+    free(kept);
+    return (int64_t)pos;
+}

@@ -101,7 +101,88 @@ __global__ __launch_bounds__(256) void ccd_unpack_b64(const unsigned char *__res
     if (bad) atomicOr(err, 1ull);
 }
 
+// ---- transport-encoded batches (ccd_encode.c; layout in include/ccdgpu.h) -> the standard
+// band-major spectra [7][n_pix][n_obs] and QA [n_pix][n_obs] of every chip, bit for bit.  One
+// wave per pixel, lane = observation: the 4-bit QA code through the chip's palette, the kept
+// (non-fill) observations' rank by ballot / mbcnt, band values gathered from the compacted
+// band columns (consecutive ranks: coalesced) and -9999 written for fill observations.  Byte
+// work at HBM speed: ~13 B read and 16 B written per observation.
+constexpr int ENC_HDR = 128;
+__device__ __forceinline__ int64_t up16(int64_t x) { return (x + 15) & ~(int64_t)15; }
+
+__global__ __launch_bounds__(256) void ccd_decode_enc(const unsigned char *__restrict__ enc, int64_t total_pix,
+                                                       int16_t *__restrict__ spectra, uint16_t *__restrict__ qa) {
+    const int64_t pix = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (pix >= total_pix) return;
+    const int l = threadIdx.x & 63;
+    const int64_t *tab = reinterpret_cast<const int64_t *>(enc);
+    const int64_t nc = tab[0];
+    const int64_t *off = tab + 1, *pixo = tab + 2 + nc;
+    int64_t lo = 0, hi = nc - 1;  // the pixel's chip (wave-uniform binary search)
+    while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (pixo[mid] <= pix) lo = mid;
+        else hi = mid - 1;
+    }
+    const unsigned char *sec = enc + off[lo];
+    const int32_t *h = reinterpret_cast<const int32_t *>(sec);
+    const int mode = h[0], n_pix = h[1], n_obs = h[2];
+    const int64_t *h64 = reinterpret_cast<const int64_t *>(sec + 48);
+    const int64_t data_off = h64[1], bstride = h64[2];
+    const int64_t p = pix - pixo[lo];
+    const int64_t plane = (int64_t)n_pix * n_obs;
+    int16_t *sp = spectra + 7 * data_off + p * n_obs;
+    uint16_t *qo = qa + data_off + p * n_obs;
+    if (mode == 0) {
+        const uint16_t *rq = reinterpret_cast<const uint16_t *>(sec + ENC_HDR) + p * n_obs;
+        const int16_t *rs = reinterpret_cast<const int16_t *>(sec + ENC_HDR + up16(2 * plane)) + p * n_obs;
+        for (int i = l; i < n_obs; i += 64) {
+            qo[i] = rq[i];
+#pragma unroll
+            for (int b = 0; b < 7; ++b) sp[(int64_t)b * plane + i] = rs[(int64_t)b * plane + i];
+        }
+        return;
+    }
+    const uint16_t *pal = reinterpret_cast<const uint16_t *>(sec + 16);
+    const uint32_t *koff = reinterpret_cast<const uint32_t *>(sec + ENC_HDR);
+    const unsigned char *q4 = sec + ENC_HDR + up16(4 * ((int64_t)n_pix + 1));
+    const int64_t rowb = (n_obs + 1) / 2;
+    const int16_t *bands = reinterpret_cast<const int16_t *>(q4 + up16((int64_t)n_pix * rowb)) + koff[p];
+    const unsigned char *qr = q4 + p * rowb;
+    int carry = 0;
+    for (int i0 = 0; i0 < n_obs; i0 += 64) {
+        const int i = i0 + l;
+        const bool in = i < n_obs;
+        const unsigned code = in ? (qr[i >> 1] >> ((i & 1) * 4)) & 15u : 0u;
+        const uint16_t q = pal[code];
+        const bool keep = in && !(q & 1u);
+        const unsigned long long km = __ballot(keep);
+        const int rank = carry + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(km >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)km, 0));
+        if (in) {
+            qo[i] = q;
+            int16_t v[7];
+#pragma unroll
+            for (int b = 0; b < 7; ++b) v[b] = (int16_t)-9999;
+            if (keep) {  // (loads under the lane's own mask: a fill lane's rank may point past the column)
+#pragma unroll
+                for (int b = 0; b < 7; ++b) v[b] = bands[b * bstride + rank];
+            }
+#pragma unroll
+            for (int b = 0; b < 7; ++b) sp[(int64_t)b * plane + i] = v[b];
+        }
+        carry += __popcll(km);
+    }
+}
+
 }  // namespace
+
+extern "C" int ccdk_decode_enc(const unsigned char *enc, int64_t total_pix, int16_t *spectra, uint16_t *qa,
+                               void *stream) {
+    if (total_pix <= 0) return 0;
+    hipLaunchKernelGGL(ccd_decode_enc, dim3((unsigned)((total_pix + 3) / 4)), dim3(256), 0, (hipStream_t)stream, enc,
+                       total_pix, spectra, qa);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 extern "C" int ccdk_unpack_b64(const unsigned char *text, int64_t text_bytes, const int64_t *offsets, int32_t n_chips,
                                int32_t n_obs, int32_t n_pix, int16_t *spectra, uint16_t *qa,

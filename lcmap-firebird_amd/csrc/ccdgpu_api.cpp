@@ -198,6 +198,7 @@ struct ccdgpu_ctx {
     DevBuf<int64_t> slot_dates[CCDGPU_UPLOAD_SLOTS];   // upload slots (ccdgpu_stage_slot / ccdgpu_run_slot)
     DevBuf<int16_t> slot_spectra[CCDGPU_UPLOAD_SLOTS];
     DevBuf<uint16_t> slot_qa[CCDGPU_UPLOAD_SLOTS];
+    DevBuf<unsigned char> slot_enc[CCDGPU_UPLOAD_SLOTS];  // transport-encoded uploads (ccdgpu_stage_slot_encoded)
     Shape slot_shape[CCDGPU_UPLOAD_SLOTS];
     ccdgpu_params slot_params[CCDGPU_UPLOAD_SLOTS];
     bool slot_ready[CCDGPU_UPLOAD_SLOTS] = {};
@@ -226,6 +227,7 @@ struct ccdgpu_ctx {
             slot_dates[i].release();
             slot_spectra[i].release();
             slot_qa[i].release();
+            slot_enc[i].release();
             if (uploaded[i]) (void)hipEventDestroy(uploaded[i]);
         }
         if (copy_stream) (void)hipStreamDestroy(copy_stream);
@@ -562,6 +564,53 @@ int ccdgpu_stage_slot_chips(ccdgpu_ctx *c, int32_t slot, const ccdgpu_params *pa
     HIPCHK(hipEventRecord(c->uploaded[slot], c->copy_stream));
     c->slot_shape[slot] = sh;
     c->slot_params[slot] = *params;  // each slot keeps its own parameters
+    c->slot_ready[slot] = true;
+    return 0;
+}
+
+int ccdgpu_stage_slot_encoded(ccdgpu_ctx *c, int32_t slot, const ccdgpu_params *params, int32_t n_chips,
+                              const int32_t *n_pix, const int32_t *n_obs, const int64_t *dates, const uint8_t *enc,
+                              int64_t enc_bytes) {
+    if (!c) return fail(CCDGPU_EINVAL, "NULL ctx");
+    if (slot < 0 || slot >= CCDGPU_UPLOAD_SLOTS)
+        return fail(CCDGPU_EINVAL, "slot must be in 0 .. " + std::to_string(CCDGPU_UPLOAD_SLOTS - 1));
+    if (!dates || !enc) return fail(CCDGPU_EINVAL, "NULL input buffer");
+    Shape sh;
+    int rc = make_shape(n_chips, n_pix, n_obs, sh);
+    if (rc || (rc = check_params(params))) return rc;
+    // the encoded batch must describe exactly these chips (the decoder trusts its headers)
+    const int64_t *tab = reinterpret_cast<const int64_t *>(enc);
+    if (enc_bytes < (int64_t)(8 * (2 * (int64_t)n_chips + 3)) || tab[0] != n_chips)
+        return fail(CCDGPU_EINVAL, "encoded batch: chip table does not match n_chips");
+    const int64_t *off = tab + 1, *pixo = tab + 2 + n_chips;
+    if (off[n_chips] > enc_bytes) return fail(CCDGPU_EINVAL, "encoded batch: longer than enc_bytes");
+    int64_t pb = 0, db = 0;
+    for (int32_t k = 0; k < n_chips; ++k) {
+        if (off[k] < 0 || off[k] + 128 > off[k + 1] || pixo[k] != pb)
+            return fail(CCDGPU_EINVAL, "encoded batch: bad chip table entry " + std::to_string(k));
+        const int32_t *h = reinterpret_cast<const int32_t *>(enc + off[k]);
+        const int64_t *h64 = reinterpret_cast<const int64_t *>(enc + off[k] + 48);
+        if ((h[0] != 0 && h[0] != 1) || h[1] != n_pix[k] || h[2] != n_obs[k] || h64[1] != db ||
+            (h[0] == 1 && (h[3] < 1 || h[3] > 16)))
+            return fail(CCDGPU_EINVAL, "encoded batch: chip " + std::to_string(k) + " header does not match its shape");
+        pb += n_pix[k];
+        db += (int64_t)n_pix[k] * n_obs[k];
+    }
+    if (pixo[n_chips] != pb) return fail(CCDGPU_EINVAL, "encoded batch: pixel total does not match");
+    HIPCHK(hipSetDevice(c->device));
+    const size_t tobs = (size_t)sh.total_obs(), tdata = (size_t)sh.total_data();
+    if ((rc = c->slot_dates[slot].ensure(tobs)) || (rc = c->slot_spectra[slot].ensure(7 * tdata)) ||
+        (rc = c->slot_qa[slot].ensure(tdata)) || (rc = c->slot_enc[slot].ensure((size_t)off[n_chips])))
+        return rc;
+    // upload on the copy stream, then decode there into the slot's standard buffers; run_slot
+    // waits for both through the slot's event
+    HIPCHK(hipMemcpyAsync(c->slot_dates[slot].p, dates, sizeof(int64_t) * tobs, hipMemcpyHostToDevice, c->copy_stream));
+    HIPCHK(hipMemcpyAsync(c->slot_enc[slot].p, enc, (size_t)off[n_chips], hipMemcpyHostToDevice, c->copy_stream));
+    if (ccdk_decode_enc(c->slot_enc[slot].p, pb, c->slot_spectra[slot].p, c->slot_qa[slot].p, c->copy_stream))
+        return fail(CCDGPU_EHIP, "ccd_decode_enc launch failed");
+    HIPCHK(hipEventRecord(c->uploaded[slot], c->copy_stream));
+    c->slot_shape[slot] = sh;
+    c->slot_params[slot] = *params;
     c->slot_ready[slot] = true;
     return 0;
 }

@@ -59,6 +59,11 @@ class OracleContext(object):
         self._results = None
 
     def stage_slot_chips(self, slot, batch, params=None):
+        import ccdgpu
+        if isinstance(batch, ccdgpu.EncodedBatch):  # the runner's transport encoding: decode as the device does
+            from encode_util import decode
+            chips = decode(batch.buf[:batch.nbytes_encoded])
+            batch = ccdgpu.ChipBatch.from_chips([(batch.chip(c)[0], s, q) for c, (s, q) in enumerate(chips)])
         self._slots[slot] = (batch, params)
 
     def run_slot(self, slot):

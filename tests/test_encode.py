@@ -1,0 +1,98 @@
+"""Transport encoding of chips for the PCIe upload (ccdgpu_encode_chips, include/ccdgpu.h): the
+encoded bytes decode -- with a numpy restatement of the device decoder (ccd_decode_enc,
+ccd_pack.hip) -- to the original spectra and QA bit for bit, for encoded and raw-fallback chips,
+and the AVX-512 VBMI2 and scalar encoders write the same bytes.  CPU only (no device)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(ROOT, 'lcmap-firebird_amd'))
+
+ccdgpu = pytest.importorskip('ccdgpu')
+from ccdgpu import synth  # noqa: E402
+
+
+from encode_util import decode  # noqa: E402
+
+
+def encode(chips, threads=3):
+    e = ccdgpu.EncodedBatch.encode(chips, threads=threads, pinned=False)
+    return e, e.buf[:e.nbytes_encoded]
+
+
+def check_roundtrip(chips, modes=None):
+    e, buf = encode(chips)
+    dec = decode(buf)
+    for (d, s, q), (ds, dq) in zip(chips, dec):
+        np.testing.assert_array_equal(ds, s)
+        np.testing.assert_array_equal(dq, q)
+    if modes is not None:
+        assert e.chip_modes() == modes
+    return e
+
+
+def test_synthetic_tile_chips_roundtrip_and_shrink():
+    cfg = synth.config(3)
+    chips = [synth.chip(cfg, c, 0, 300) for c in (0, 1, 2)]  # base cadence and sidelap
+    e = check_roundtrip(chips, [1, 1, 1])
+    raw = sum(s.nbytes + q.nbytes for _, s, q in chips)
+    assert e.nbytes_encoded < 0.9 * raw
+
+
+def test_masked_and_change_dense_configs_roundtrip():
+    for which in (2, 4, 5):
+        cfg = synth.config(which)
+        check_roundtrip([synth.chip(cfg, 7, 0, 128), synth.chip(cfg, 8, 0, 77)])
+
+
+def test_raw_fallbacks_and_edge_shapes():
+    rng = np.random.default_rng(5)
+    n = 33  # odd observation count: the last QA byte holds one code
+    d = np.arange(n, dtype=np.int64) * 16 + 730000
+    # more than 16 distinct QA words -> raw
+    q_many = rng.integers(2, 4000, size=(5, n)).astype(np.uint16) & ~np.uint16(1)
+    s_many = rng.integers(-100, 10000, size=(7, 5, n)).astype(np.int16)
+    # a fill observation (QA bit 0) whose bands are not all -9999 -> raw
+    q_bad = np.full((3, n), 66, dtype=np.uint16)
+    q_bad[1, 4] = 1
+    s_bad = rng.integers(0, 5000, size=(7, 3, n)).astype(np.int16)
+    s_bad[:, 1, 4] = -9999
+    s_bad[3, 1, 4] = 17
+    # all observations fill (nothing kept), one pixel
+    q_fill = np.ones((1, n), dtype=np.uint16)
+    s_fill = np.full((7, 1, n), -9999, dtype=np.int16)
+    # a single observation
+    q_one = np.array([[322]], dtype=np.uint16)
+    s_one = np.array([[[5]], [[6]], [[7]], [[8]], [[9]], [[10]], [[11]]], dtype=np.int16)
+    check_roundtrip([(d, s_many, q_many), (d, s_bad, q_bad), (d, s_fill, q_fill), (d[:1], s_one, q_one)],
+                    [0, 0, 1, 1])
+
+
+def test_vector_and_scalar_encoders_write_the_same_bytes():
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); import ccdgpu; from ccdgpu import synth; "
+            "cfg = synth.config(3); chips = [synth.chip(cfg, c, 0, 97) for c in (0, 1)]; "
+            "e = ccdgpu.EncodedBatch.encode(chips, threads=2, pinned=False); "
+            "sys.stdout.buffer.write(bytes([int(ccdgpu.encode_vector_path())]) + e.buf[:e.nbytes_encoded].tobytes())"
+            % os.path.join(ROOT, 'lcmap-firebird_amd'))
+    outs = {}
+    for scalar in ('0', '1'):
+        env = dict(os.environ, CCDGPU_ENCODE_SCALAR=scalar)
+        outs[scalar] = subprocess.run([sys.executable, '-c', code], env=env, capture_output=True, check=True).stdout
+    assert outs['1'][0] == 0
+    if outs['0'][0] == 0:
+        pytest.skip('no AVX-512 VBMI2 on this CPU: only the scalar encoder ran')
+    assert outs['0'][1:] == outs['1'][1:]
+
+
+def test_encode_rejects_a_short_buffer():
+    cfg = synth.config(3)
+    d, s, q = synth.chip(cfg, 0, 0, 10)
+    e = ccdgpu.EncodedBatch([10], [d.shape[0]], pinned=False)
+    e.buf = e.buf[:100]
+    with pytest.raises(ValueError):
+        e.fill([(d, s, q)])

@@ -1,0 +1,55 @@
+"""Transport-encoded uploads on the GPU (ccdgpu_stage_slot_encoded + ccd_decode_enc): the device
+decode of an encoded batch equals the raw upload bit for bit -- encoded and raw-fallback chips,
+both cadences, masked QA -- and detection of it returns the same segments."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def chips():
+    from ccdgpu import synth
+    out = [synth.chip(synth.config(3), 0, 0, 200), synth.chip(synth.config(3), 1, 0, 150),
+           synth.chip(synth.config(4), 2, 0, 120)]
+    # a chip with more than 16 distinct QA words (raw), from a C2 chip with shuffled clear words
+    d, s, q = synth.chip(synth.config(2), 3, 0, 90)
+    q = q.copy()
+    clear = (q & 1) == 0
+    rng = np.random.default_rng(9)
+    q[clear] = np.where(rng.random(int(clear.sum())) < 0.5, q[clear], q[clear] | (rng.integers(0, 8, int(clear.sum())) << 11).astype(np.uint16))
+    out.append((d, s, q))
+    # a fill observation with data in a band (raw)
+    d, s, q = synth.chip(synth.config(3), 4, 0, 60)
+    s = s.copy()
+    fi = np.argwhere((q & 1) == 1)[0]
+    s[2, fi[0], fi[1]] = 123
+    out.append((d, s, q))
+    return out
+
+
+def test_encoded_upload_decodes_to_the_raw_inputs_and_detects_the_same():
+    import ccdgpu
+    cs = chips()
+    raw = ccdgpu.ChipBatch.from_chips(cs, pinned=True)
+    enc = ccdgpu.EncodedBatch.encode(cs, threads=4)
+    assert enc.chip_modes() == [1, 1, 1, 0, 0]
+    assert enc.nbytes_encoded < raw.spectra.nbytes + raw.qa.nbytes
+    ctx = ccdgpu.Context(0)
+    try:
+        ctx.stage_slot_chips(0, raw)
+        ctx.run_slot(0)
+        s0, q0 = ctx.staged_inputs()
+        r0 = [ctx.fetch(c) for c in range(len(cs))]
+        ctx.stage_slot_encoded(1, enc)
+        ctx.run_slot(1)
+        s1, q1 = ctx.staged_inputs()
+        r1 = [ctx.fetch(c) for c in range(len(cs))]
+    finally:
+        ctx.close()
+    np.testing.assert_array_equal(s1, np.asarray(raw.spectra))
+    np.testing.assert_array_equal(q1, np.asarray(raw.qa))
+    np.testing.assert_array_equal(s0, s1)
+    np.testing.assert_array_equal(q0, q1)
+    for a, b in zip(r0, r1):
+        assert a.segments.tobytes() == b.segments.tobytes()
+        assert np.array_equal(a.procedure, b.procedure) and np.array_equal(a.mask, b.mask)

@@ -1,8 +1,9 @@
 """The tile driver on the GPU (ccdc.runner.changedetection; reference core.changedetection,
 ccdc/core.py:78-123): chips of the reference tile grid (test/data/tile_response.json) with
-synthetic ARD of both cadences, two contexts per GPU with double-buffered pinned uploads, device
-row packing, per-chip rows gathered -- checked against rows restated from the C oracle, and
-byte-identical however the chips are batched."""
+synthetic ARD of both cadences, two contexts per GPU with pinned uploads in the transport
+encoding, device row packing, per-chip rows gathered -- checked against rows restated from the C
+oracle, and byte-identical however the chips are batched and whether they are uploaded encoded
+or raw."""
 import json
 import os
 
@@ -34,11 +35,11 @@ def source(pos):
     return ccdgpu.ChipBatch.from_chips([chip(p) for p in pos], pinned=True)
 
 
-def run(contexts, batch_chips):
+def run(contexts, batch_chips, encode=True):
     from ccdc import runner
     sink = runner.SummarySink(keep_rows=True)
     res = runner.changedetection(tile(), source, device=0, contexts=contexts, batch_chips=batch_chips,
-                                 number=N_CHIPS, sink=sink)
+                                 number=N_CHIPS, sink=sink, encode=encode)
     return res, sink
 
 
@@ -62,3 +63,6 @@ def test_tile_runner_rows_match_oracle_and_batching():
         assert np.array_equal(mask, u.mask.astype(np.int8)), p
     res2, _ = run(1, 5)
     assert [c['digest'] for c in res2['chips']] == [c['digest'] for c in res['chips']]
+    # the runner's default upload is the transport encoding: raw uploads give the same rows
+    res3, _ = run(2, 4, encode=False)
+    assert [c['digest'] for c in res3['chips']] == [c['digest'] for c in res['chips']]
