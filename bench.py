@@ -79,7 +79,10 @@ def parse():
     ap.add_argument('--tile-copy-threads', type=int, default=4, help='host threads per pool-chip copy in the tile leg source (3 contexts x 4 within the box\'s 16-CPU quota)')
     ap.add_argument('--tile-no-numa', action='store_true', help='tile leg: leave host threads unbound (A/B)')
     ap.add_argument('--tile-no-encode', action='store_true',
-                    help='tile leg: upload raw chips (pool copies into pinned batches) instead of the lossless transport encoding (A/B)')
+                    help='tile leg: upload raw chips (pool copies into pinned batches) instead of the transport encoding (A/B)')
+    ap.add_argument('--tile-encode', choices=('unread', 'lossless'), default='unread',
+                    help='tile leg transport encoding: drop the band values of fill/cloud/shadow observations '
+                         '(never read by the detection; default) or only of fill observations (lossless)')
     ap.add_argument('--tile-depth', type=int, default=2, help='batches each tile-leg context keeps uploaded ahead')
     ap.add_argument('--share-device', action='store_true',
                     help='rehearsal only: ranks beyond the device count share devices (LOCAL_RANK mod count)')
@@ -440,7 +443,7 @@ def tile_leg(args, cfg, rank, world, device, dist):
     if encode:
         # the runner's transport encoding (ccdc.runner.EncodingSource): each batch is encoded from
         # the pool chips' own arrays into pinned buffers by the fetch thread and decoded on the GPU
-        esrc = runner.EncodingSource(src, threads=args.tile_copy_threads)
+        esrc = runner.EncodingSource(src, threads=args.tile_copy_threads, drop=args.tile_encode)
         esrc.prefill(n_inflight, B, 10000, src.max_obs)
         src_timed = src_warm = esrc
     else:
@@ -487,7 +490,8 @@ def tile_leg(args, cfg, rank, world, device, dist):
         enc_stats = {'upload_bytes_raw_rank0': raw_b, 'upload_bytes_sent_rank0': sent_b,
                      'sent_over_raw': round(sent_b / raw_b, 4) if raw_b else None,
                      'encode_thread_seconds_rank0': round(esrc.encode_seconds - enc0[2], 3),
-                     'encoder_avx512_vbmi2': bool(ccdgpu.encode_vector_path())}
+                     'encoder_avx512_vbmi2': bool(ccdgpu.encode_vector_path()), 'drop': args.tile_encode,
+                     'drop_bits': esrc.drop_bits, 'strict_bits': esrc.strict_bits}
     for c in ctxs:
         c.close()
     src.close()
@@ -518,8 +522,11 @@ def tile_leg(args, cfg, rank, world, device, dist):
                     'position-dependent multiple of 16 days; generate mode: every chip generated on the GPU into pinned '
                     'host memory); %s; H2D upload overlapped with detection, device row packing, D2H of rows, gather of '
                     'per-chip summaries on rank 0' % (args.tile_pool,
-                    'each batch losslessly transport-encoded by the runner\'s fetch threads straight from the chip '
-                    'arrays into pinned buffers (fill bands dropped, QA as palette codes) and decoded on the GPU'
+                    'each batch transport-encoded by the runner\'s fetch threads straight from the chip arrays into '
+                    'pinned buffers (QA as palette codes; band values of fill%s observations not sent -- %s) and '
+                    'decoded on the GPU' % ('/cloud/shadow' if args.tile_encode == 'unread' else '',
+                                            'never read by the detection, results identical'
+                                            if args.tile_encode == 'unread' else 'lossless')
                     if encode else 'chips copied into pinned batches by the runner\'s fetch threads, uploaded raw')}
 
 

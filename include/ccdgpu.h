@@ -209,18 +209,21 @@ int ccdgpu_stage_slot(ccdgpu_ctx *ctx, int32_t slot, const ccdgpu_params *params
                       int32_t n_obs, const int64_t *dates, const int16_t *spectra, const uint16_t *qa);
 int ccdgpu_run_slot(ccdgpu_ctx *ctx, int32_t slot, double *kernel_seconds);
 
-/* Transport-encoded uploads (lossless; no reference counterpart -- the tile path's PCIe link is
- * its bound).  ccdgpu_encode_chips packs chips given as per-chip pointers
- * (spectra [7][n_pix][n_obs] int16, qa [n_pix][n_obs] uint16, the ccdgpu_stage_chips layout of
- * one chip) into `out` (>= ccdgpu_encoded_bound bytes; pinned for an asynchronous upload) and
- * returns the bytes written (< 0 on bad arguments).  Per chip: a fill observation (QA bit 0)
- * whose 7 bands are all -9999 sends no band values, and QA words become 4-bit indices into the
- * chip's palette when it has at most 16 distinct words; any other chip is sent raw.  Layout:
+/* Transport-encoded uploads (no reference counterpart -- the tile path's PCIe link is its bound,
+ * DESIGN.md §5).  ccdgpu_encode_chips packs chips given as per-chip pointers (spectra
+ * [7][n_pix][n_obs] int16, qa [n_pix][n_obs] uint16, the ccdgpu_stage_chips layout of one chip)
+ * into `out` (>= ccdgpu_encoded_bound bytes; pinned for an asynchronous upload) and returns the
+ * bytes written (< 0 on bad arguments).  Per chip: an observation whose QA word has any of
+ * `drop_bits` set sends no band values (the decoder writes -9999); if it also has any of
+ * `strict_bits` (a subset of drop_bits) its 7 bands must all be -9999 or the chip is sent raw --
+ * drop_bits = strict_bits = the fill bit is lossless; adding the cloud and shadow bits drops
+ * only values the detection never reads (ccd_encode.c); QA words become 4-bit indices into the
+ * chip's palette when it has at most 16 distinct words, else the chip is sent raw.  Layout:
  *   int64 n_chips; int64 chip_off[n_chips + 1] (bytes from `out`, 256-aligned);
  *   int64 chip_pix[n_chips + 1] (pixel prefix); chip sections:
  *   header (128 B): int32 mode (0 raw, 1 encoded), n_pix, n_obs, n_pal; uint16 pal[16];
  *                   int64 kept, data_off (the chip's offset in the standard layout), band_stride,
- *                   pix_base
+ *                   pix_base; uint32 drop_bits
  *   mode 1: uint32 kept_off[n_pix + 1]; uint8 qa4[n_pix][(n_obs + 1) / 2] (low nibble = even
  *           observation); int16 bands[7][band_stride] (kept observations, pixel-major) -- each
  *           part 16-byte aligned
@@ -230,7 +233,8 @@ int ccdgpu_run_slot(ccdgpu_ctx *ctx, int32_t slot, double *kernel_seconds);
  * with ccdgpu_run_slot.  ccdgpu_encode_vector_path: 1 if the encoder uses AVX-512 VBMI2. */
 int64_t ccdgpu_encoded_bound(int32_t n_chips, const int32_t *n_pix, const int32_t *n_obs);
 int64_t ccdgpu_encode_chips(int32_t n_chips, const int32_t *n_pix, const int32_t *n_obs, const int16_t *const *spectra,
-                            const uint16_t *const *qa, uint8_t *out, int64_t out_cap, int32_t threads);
+                            const uint16_t *const *qa, uint8_t *out, int64_t out_cap, int32_t threads,
+                            uint16_t drop_bits, uint16_t strict_bits);
 int32_t ccdgpu_encode_vector_path(void);
 int ccdgpu_stage_slot_encoded(ccdgpu_ctx *ctx, int32_t slot, const ccdgpu_params *params, int32_t n_chips,
                               const int32_t *n_pix, const int32_t *n_obs, const int64_t *dates, const uint8_t *enc,

@@ -185,17 +185,29 @@ class ParquetSink(object):
 # --------------------------------------------------------------------------- transport encoding
 class EncodingSource(object):
     """Source wrapper for the upload: every batch the wrapped ``source`` returns is encoded into a
-    pinned ``ccdgpu.EncodedBatch`` (lossless: fill observations' -9999 bands dropped, QA words as
-    4-bit palette codes; chips that do not fit go raw -- include/ccdgpu.h) by ``threads`` host
-    threads in the fetch thread, and decoded on the device after the upload.  On the tile mix it
-    sends ~18 % fewer bytes over the PCIe link, which bounds the tile.  The encode
+    pinned ``ccdgpu.EncodedBatch`` by ``threads`` host threads in the fetch thread, and decoded on
+    the device after the upload (include/ccdgpu.h, ccd_encode.c).  ``drop='unread'`` (default):
+    observations whose QA word has the fill, cloud or shadow bit send no band values -- no pyccd
+    procedure keeps those classes, so the detection never reads them and its results are the
+    same (``ccdgpu.unread_drop_bits(params)``); ``drop='lossless'``: only fill observations
+    holding -9999, so the device inputs equal the raw ones bit for bit.  QA words travel as 4-bit
+    palette codes either way; chips that do not fit go raw.  On the tile mix 'unread' sends ~47 %
+    of the raw bytes, 'lossless' ~82 %: the PCIe link bounds the tile.  The encode
     is the pass every fetched chip needs anyway to reach pinned memory: a source with a
     ``views(positions)`` method hands over its own arrays (no copy before the encode); otherwise
     its batch is encoded and released at once.  ``bytes_raw`` / ``bytes_sent`` count the traffic."""
 
-    def __init__(self, source, threads=4, pinned=None):
+    def __init__(self, source, threads=4, pinned=None, drop='unread', params=None):
+        import ccdgpu
         self.source = source
         self.threads = int(threads)
+        if drop == 'unread':
+            self.drop_bits, self.strict_bits = ccdgpu.unread_drop_bits(params)
+        elif drop == 'lossless':
+            self.drop_bits = self.strict_bits = 1
+        else:
+            raise ValueError("drop must be 'unread' or 'lossless', got %r" % (drop,))
+        self.drop = drop
         self.pinned = pinned  # None: pinned when the runtime can page-lock (a GPU host), else pageable
         self._free = []
         self._lock = threading.Lock()
@@ -226,7 +238,7 @@ class EncodingSource(object):
             st = (need, self._storage(need))
         b = ccdgpu.EncodedBatch(n_pix, n_obs, storage=st[1])
         b._enc_storage = st
-        b.fill(chips, self.threads)
+        b.fill(chips, self.threads, self.drop_bits, self.strict_bits)
         if raw is not None:
             release = getattr(self.source, 'release', None)
             if release is not None:
@@ -398,9 +410,10 @@ def detect_tile(xys, source, queue, device=0, contexts=3, batch_chips=8, params=
     and this process's statistics.  ``upload_depth``: batches each context keeps uploaded or
     uploading ahead of the one it detects (1 .. ccdgpu.UPLOAD_SLOTS - 1).  ``tail_chips``: once
     fewer positions than this remain in the queue, workers pull quarter batches (default: two
-    full batches per context of this process).  ``encode``: upload every batch in the lossless
-    transport encoding (EncodingSource, ``encode_threads`` host threads per fetch) instead of
-    raw -- ``source`` may then also be an EncodingSource already (its counters are reported)."""
+    full batches per context of this process).  ``encode``: upload every batch in the transport
+    encoding (EncodingSource, ``encode_threads`` host threads per fetch; True = its 'unread'
+    setting, 'lossless' = lossless) instead of raw -- ``source`` may then also be an
+    EncodingSource already (its counters are reported)."""
     from ccdgpu import UPLOAD_SLOTS
     if not 1 <= int(upload_depth) <= UPLOAD_SLOTS - 1:
         raise ValueError('upload_depth must be in 1 .. %d (ccdgpu.UPLOAD_SLOTS - 1), got %r' % (UPLOAD_SLOTS - 1, upload_depth))
@@ -412,7 +425,8 @@ def detect_tile(xys, source, queue, device=0, contexts=3, batch_chips=8, params=
         import ccdgpu
         context_factory = ccdgpu.Context
     if encode and not isinstance(source, EncodingSource):
-        source = EncodingSource(source, threads=encode_threads)
+        source = EncodingSource(source, threads=encode_threads, drop='lossless' if encode == 'lossless' else 'unread',
+                                params=params)
     sink = sink if sink is not None else SummarySink()
     # per-phase host seconds summed over the workers: source (ARD fetch), stage (upload call),
     # device (run_slot: waits for the upload, detects), fetch (row packing + D2H), sink

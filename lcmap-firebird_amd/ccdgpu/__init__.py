@@ -44,7 +44,7 @@ def _declare(L):
         L.ccdgpu_encoded_bound.argtypes = [c.c_int32, c.c_void_p, c.c_void_p]
         L.ccdgpu_encoded_bound.restype = c.c_int64
         L.ccdgpu_encode_chips.argtypes = [c.c_int32, c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p,
-                                          c.c_int64, c.c_int32]
+                                          c.c_int64, c.c_int32, c.c_uint16, c.c_uint16]
         L.ccdgpu_encode_chips.restype = c.c_int64
         L.ccdgpu_encode_vector_path.restype = c.c_int32
         L.ccdgpu_stage_slot_encoded.argtypes = [c.c_void_p, c.c_int32, c.c_void_p, c.c_int32, c.c_void_p, c.c_void_p,
@@ -264,10 +264,13 @@ class EncodedBatch(ChipBatch):
     def set_chip(self, c, dates, spectra, qa):
         raise TypeError('EncodedBatch holds encoded chips: build it with EncodedBatch.encode')
 
-    def fill(self, chips, threads=4):
+    def fill(self, chips, threads=4, drop_bits=1, strict_bits=1):
         """Encode chips [(dates [n], spectra [7][n_pix][n] int16, qa [n_pix][n] uint16), ...]
         (any C-contiguous arrays: pinned batch views, or a source's own arrays -- nothing else is
-        copied) into this batch; returns the encoded bytes."""
+        copied) into this batch; returns the encoded bytes.  ``drop_bits`` / ``strict_bits``:
+        QA bits whose observations send no band values / must hold -9999 (include/ccdgpu.h; the
+        default, the fill bit for both, is lossless; ``unread_drop_bits(params)`` gives the bits of
+        observations the detection never reads)."""
         chips = list(chips)
         if len(chips) != self.n_chips:
             raise ValueError('%d chips for a batch of %d' % (len(chips), self.n_chips))
@@ -287,17 +290,18 @@ class EncodedBatch(ChipBatch):
             keep.append((s, q))
         n = int(lib().ccdgpu_encode_chips(self.n_chips, self.n_pix.ctypes.data, self.n_obs.ctypes.data,
                                           ctypes.cast(sp, ctypes.c_void_p), ctypes.cast(qp, ctypes.c_void_p),
-                                          self.buf.ctypes.data, self.buf.size, int(threads)))
+                                          self.buf.ctypes.data, self.buf.size, int(threads), int(drop_bits),
+                                          int(strict_bits)))
         if n < 0:
             raise ValueError('ccdgpu_encode_chips failed (%d)' % n)
         self.nbytes_encoded = n
         return n
 
     @classmethod
-    def encode(cls, chips, threads=4, storage=None, pinned=True):
+    def encode(cls, chips, threads=4, storage=None, pinned=True, drop_bits=1, strict_bits=1):
         chips = list(chips)
         b = cls([c[2].shape[0] for c in chips], [c[0].shape[0] for c in chips], storage=storage, pinned=pinned)
-        b.fill(chips, threads)
+        b.fill(chips, threads, drop_bits, strict_bits)
         return b
 
     def chip_modes(self):
@@ -315,6 +319,24 @@ def encode_storage(max_chips, max_pix, max_obs, pinned=True):
     bound = int(lib().ccdgpu_encoded_bound(n, np_.ctypes.data, no.ctypes.data))
     alloc = pinned_empty if pinned else np.empty
     return alloc((n * int(max_obs),), np.int64), alloc((bound,), np.uint8)
+
+
+def unread_drop_bits(params=None):
+    """(drop_bits, strict_bits) for the transport encoding that drops every band value the
+    detection never reads: observations whose QA word has the fill, cloud or shadow bit (qabitval
+    classes them as fill / cloud / shadow whatever else is set, and no procedure keeps those
+    classes); fill observations stay strict (their bands must be -9999).  For non-bit-packed QA
+    (class values, not bits) only the lossless (fill bit 0) setting applies."""
+    p = params if isinstance(params, abi.Params) else abi.params_from_dict(params)
+    if not p.qa_bitpacked:
+        return 0, 0
+    bits = [int(p.qa_fill), int(p.qa_cloud), int(p.qa_shadow)]
+    if any(b < 0 or b > 15 for b in bits):
+        return 0, 0  # (bits outside a 16-bit word: nothing dropped)
+    drop = 0
+    for b in bits:
+        drop |= 1 << b
+    return drop, 1 << int(p.qa_fill)
 
 
 def encode_vector_path():

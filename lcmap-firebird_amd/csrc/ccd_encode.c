@@ -1,17 +1,22 @@
-/* ccd_encode.c -- lossless transport encoding of ARD chips for the PCIe upload (host side).
+/* ccd_encode.c -- transport encoding of ARD chips for the PCIe upload (host side).
  *
  * The tile path is bound by the host-to-device link (16 bytes per observation: 7 int16 bands +
- * a uint16 QA word).  Two properties of Landsat ARD make those bytes compressible
- * without loss, and both are checked per chip, so the encoding is exact for any input:
- *   - a fill observation (pixel_qa bit 0, qa.py's fill bit) carries the ARD fill value -9999 in
- *     every band: its band values are dropped and restored on the device;
+ * a uint16 QA word).  The encoding sends less of it:
+ *   - the band values of an observation whose QA word has any of `drop_bits` set are not sent;
+ *     the device writes -9999 (the ARD fill value) in their place.  With drop_bits = the fill bit
+ *     (and strict_bits = the same: such an observation must hold -9999 in every band, or its chip
+ *     goes raw) the encoding is lossless.  With the fill, cloud and shadow bits it drops values
+ *     the detection never reads: pyccd's procedures (qa.standard_procedure_filter and the snow
+ *     and insufficient-clear filters) keep only clear / water (/ snow) observations -- the class
+ *     qabitval gives a word, fill > cloud > shadow > snow > water > clear -- so a word with the
+ *     fill, cloud or shadow bit is never in a processing mask and its band values never enter a
+ *     test or a fit (px_setup in ccd_kernels.hip: keep = class clear or water (or snow) and the
+ *     range tests), and the results are the same (tests/test_gpu_encode.py, test_gpu_tile.py);
  *   - a chip's QA words take a handful of distinct values: each becomes a 4-bit index into a
- *     16-entry palette.
- * A chip with a fill observation whose bands are not all -9999, or with more than 16 distinct QA
- * words, is sent raw (mode 0).  The device decoder (ccd_decode_enc in ccd_pack.hip) rebuilds the
- * standard band-major [7][n_pix][n_obs] spectra and [n_pix][n_obs] QA of every chip bit for bit,
- * so detection runs unchanged (tests/test_encode.py: round trips against a numpy decoder;
- * tests/test_gpu_encode.py: device decode == raw upload).  Layout: include/ccdgpu.h.
+ *     16-entry palette (a chip with more distinct words is sent raw, mode 0).
+ * The device decoder (ccd_decode_enc in ccd_pack.hip) rebuilds the standard band-major
+ * [7][n_pix][n_obs] spectra and [n_pix][n_obs] QA of every chip (tests/test_encode.py: round
+ * trips against a numpy decoder).  Layout: include/ccdgpu.h.
  *
  * The encode replaces the copy into pinned memory that every upload from a fetched (pageable)
  * chip needs anyway; it runs one pass over the QA words (counts, palette, fill check) and one
@@ -53,14 +58,16 @@ int64_t ccdgpu_encoded_bound(int32_t n_chips, const int32_t *n_pix, const int32_
 }
 
 /* ---- band compaction: dst[k++] = src[i] for the observations kept (keep[i] = 1); *bad is set
- * when a dropped (fill) observation's value is not -9999 (the chip then goes raw) */
-static size_t compact_scalar(const int16_t *src, const uint8_t *keep, int n, int16_t *dst, int *bad) {
+ * when a dropped observation that must hold the fill value (strict[i] = 1) holds another one
+ * (the chip then goes raw) */
+static size_t compact_scalar(const int16_t *src, const uint8_t *keep, const uint8_t *strict, int n, int16_t *dst,
+                             int *bad) {
     size_t k = 0;
     int b = 0;
     for (int i = 0; i < n; ++i) {
         dst[k] = src[i];
         k += keep[i];
-        b |= !keep[i] & (src[i] != -9999);
+        b |= strict[i] & (src[i] != -9999);
     }
     *bad |= b;
     return k;
@@ -68,11 +75,13 @@ static size_t compact_scalar(const int16_t *src, const uint8_t *keep, int n, int
 
 #if defined(__x86_64__)
 #include <immintrin.h>
-/* the same with AVX-512 VBMI2, 32 observations at a time; m[] = keep bit masks.  The kept values
+/* the same with AVX-512 VBMI2, 32 observations at a time; m[] = keep bit masks, sm[] = the strict
+ * observations' bit masks.  The kept values
  * are compressed in a register and written with a masked store of exactly their count (a
  * compress with a memory destination is microcoded and slow on Zen 4/5). */
 __attribute__((target("avx512f,avx512bw,avx512vbmi2"))) static size_t compact_vbmi2(const int16_t *src,
-                                                                                   const uint32_t *m, int n,
+                                                                                   const uint32_t *m,
+                                                                                   const uint32_t *sm, int n,
                                                                                    int16_t *dst, int *bad) {
     size_t k = 0;
     int i = 0, w = 0;
@@ -84,7 +93,7 @@ __attribute__((target("avx512f,avx512bw,avx512vbmi2"))) static size_t compact_vb
         _mm512_mask_storeu_epi16(dst + k, (__mmask32)(c == 32 ? 0xFFFFFFFFu : (1u << c) - 1u),
                                  _mm512_maskz_compress_epi16((__mmask32)m[w], v));
         k += (size_t)c;
-        nb |= _mm512_mask_cmpneq_epi16_mask((__mmask32)~m[w], v, fillv);
+        nb |= _mm512_mask_cmpneq_epi16_mask((__mmask32)sm[w], v, fillv);
     }
     if (i < n) {
         const __mmask32 tail = (__mmask32)((1ull << (n - i)) - 1ull);
@@ -92,7 +101,7 @@ __attribute__((target("avx512f,avx512bw,avx512vbmi2"))) static size_t compact_vb
         const int c = __builtin_popcount(m[w] & tail);
         _mm512_mask_storeu_epi16(dst + k, (__mmask32)((1u << c) - 1u), _mm512_maskz_compress_epi16((__mmask32)(m[w] & tail), v));
         k += (size_t)c;
-        nb |= _mm512_mask_cmpneq_epi16_mask((__mmask32)(~m[w] & tail), v, fillv);
+        nb |= _mm512_mask_cmpneq_epi16_mask((__mmask32)(sm[w] & tail), v, fillv);
     }
     *bad |= nb != 0;
     return k;
@@ -103,9 +112,11 @@ __attribute__((target("avx512f,avx512bw,avx512vbmi2"))) static size_t compact_vb
  * bytes with one down-convert. */
 __attribute__((target("avx512f,avx512bw,avx512vl,avx512vbmi2"))) static void qa_codes_avx512(const uint16_t *q, int n,
                                                                                    const uint16_t *pal, int npal,
-                                                                                   uint8_t *r, uint32_t *km) {
+                                                                                   uint16_t drop, uint16_t strict,
+                                                                                   uint8_t *r, uint32_t *km,
+                                                                                   uint32_t *sm) {
     int i = 0, w = 0;
-    const __m512i one = _mm512_set1_epi16(1);
+    const __m512i dropv = _mm512_set1_epi16((short)drop), strictv = _mm512_set1_epi16((short)strict);
     for (; i < n; i += 32, ++w) {
         const __mmask32 lm = n - i >= 32 ? (__mmask32)0xFFFFFFFFu : (__mmask32)((1u << (n - i)) - 1u);
         const __m512i v = _mm512_maskz_loadu_epi16(lm, (const void *)(q + i));
@@ -113,13 +124,39 @@ __attribute__((target("avx512f,avx512bw,avx512vl,avx512vbmi2"))) static void qa_
         for (int j = 1; j < npal; ++j)
             code = _mm512_mask_mov_epi16(code, _mm512_cmpeq_epi16_mask(v, _mm512_set1_epi16((short)pal[j])),
                                          _mm512_set1_epi16((short)j));
-        km[w] = (uint32_t)(_mm512_testn_epi16_mask(v, one) & lm);
+        km[w] = (uint32_t)(_mm512_testn_epi16_mask(v, dropv) & lm);
+        sm[w] = (uint32_t)(_mm512_test_epi16_mask(v, strictv) & lm);
         const __m512i pr = _mm512_or_si512(_mm512_and_si512(code, _mm512_set1_epi32(0xF)),
                                            _mm512_and_si512(_mm512_srli_epi32(code, 12), _mm512_set1_epi32(0xF0)));
         const __m128i bytes = _mm512_cvtepi32_epi8(pr);
         const int nb = (n - i >= 32 ? 32 : n - i + 1) / 2;  /* bytes of this chunk's codes */
         _mm_mask_storeu_epi8(r + (i >> 1), (__mmask16)(nb == 16 ? 0xFFFFu : (1u << nb) - 1u), bytes);
     }
+}
+/* pass 1 of one pixel's QA row, vector path: dropped count, and every word not yet in the thread's
+ * list s_pal (compared 32 at a time against the list; the rare new word is added) */
+__attribute__((target("avx512f,avx512bw,avx512vl,avx512vbmi2"))) static uint32_t qa_scan_avx512(const uint16_t *q,
+                                                                                               int n, uint16_t drop,
+                                                                                               uint16_t *s_pal,
+                                                                                               int *s_npal) {
+    uint32_t fill = 0;
+    const __m512i one = _mm512_set1_epi16((short)drop);
+    int np = *s_npal;
+    for (int i = 0; i < n; i += 32) {
+        const __mmask32 lm = n - i >= 32 ? (__mmask32)0xFFFFFFFFu : (__mmask32)((1u << (n - i)) - 1u);
+        const __m512i v = _mm512_maskz_loadu_epi16(lm, (const void *)(q + i));
+        fill += (uint32_t)__builtin_popcount(_mm512_test_epi16_mask(v, one) & lm);
+        __mmask32 un = lm;
+        for (int j = 0; j < np && un; ++j) un &= ~_mm512_cmpeq_epi16_mask(v, _mm512_set1_epi16((short)s_pal[j]));
+        while (un) {
+            const uint16_t w = q[i + __builtin_ctz(un)];
+            if (np < 17) s_pal[np++] = w;
+            un &= ~_mm512_cmpeq_epi16_mask(v, _mm512_set1_epi16((short)w));
+            if (np >= 17) un = 0;  /* more than a palette: the chip goes raw */
+        }
+    }
+    *s_npal = np;
+    return fill;
 }
 static int have_vbmi2(void) {
     static int v = -1;
@@ -139,7 +176,9 @@ int32_t ccdgpu_encode_vector_path(void) { return have_vbmi2(); }
 /* per-thread pass-1 state: the QA words seen (a 65536-bit set), a fill observation with a band
  * value other than -9999 */
 typedef struct {
-    uint8_t seen[65536];  /* (byte flags: independent stores, no read-modify-write chain) */
+    uint8_t seen[65536];  /* scalar path: byte flags (independent stores, no read-modify-write chain) */
+    uint16_t pal[17];     /* vector path: the distinct words met so far (17 = more than a palette holds) */
+    int npal;
     int bad_fill;
 } pass1_t;
 
@@ -168,7 +207,8 @@ static size_t encode_raw(int32_t n_pix, int32_t n_obs, const int16_t *spectra, c
 
 /* one chip into sec (room for the larger of its two modes); returns the section's bytes */
 static size_t encode_chip(int32_t n_pix, int32_t n_obs, const int16_t *spectra, const uint16_t *qa, int64_t pix_base,
-                          int64_t data_off, uint8_t *sec, int threads, uint32_t *kept_scratch) {
+                          int64_t data_off, uint8_t *sec, int threads, uint32_t *kept_scratch, uint16_t drop,
+                          uint16_t strict) {
     const size_t plane = (size_t)n_pix * (size_t)n_obs;
     int nt = threads > 0 ? threads : 1;
     if (nt > 64) nt = 64;
@@ -179,7 +219,8 @@ static size_t encode_chip(int32_t n_pix, int32_t n_obs, const int16_t *spectra, 
         free(lut);
         return 0;
     }
-    /* pass 1: kept counts, distinct QA words, fill observations' band values */
+    const int vec1 = have_vbmi2();
+    /* pass 1: kept counts, distinct QA words */
 #pragma omp parallel for schedule(static) num_threads(nt)
     for (int32_t p = 0; p < n_pix; ++p) {
 #ifdef _OPENMP
@@ -189,10 +230,17 @@ static size_t encode_chip(int32_t n_pix, int32_t n_obs, const int16_t *spectra, 
 #endif
         const uint16_t *q = qa + (size_t)p * n_obs;
         uint32_t fill = 0;
-        for (int32_t i = 0; i < n_obs; ++i) {
-            const uint16_t v = q[i];
-            s->seen[v] = 1;
-            fill += v & 1u;
+#if defined(__x86_64__)
+        if (vec1) {
+            fill = qa_scan_avx512(q, n_obs, drop, s->pal, &s->npal);
+        } else
+#endif
+        {
+            for (int32_t i = 0; i < n_obs; ++i) {
+                const uint16_t v = q[i];
+                s->seen[v] = 1;
+                fill += (v & drop) != 0;
+            }
         }
         kept_scratch[p] = (uint32_t)n_obs - fill;
     }
@@ -200,6 +248,11 @@ static size_t encode_chip(int32_t n_pix, int32_t n_obs, const int16_t *spectra, 
     uint16_t palv[16];
     int npal = 0;
     for (int t = 0; t < nt; ++t) bad |= st[t].bad_fill;
+    if (vec1)  /* the threads' word lists into the byte set the scalar path fills */
+        for (int t = 0; t < nt; ++t)
+            for (int j = 0; j < st[t].npal; ++j) st[t].seen[st[t].pal[j]] = 1;
+    for (int t = 0; t < nt; ++t)
+        if (st[t].npal > 16) bad = 1;  /* (vector path: one thread alone met more than 16 words) */
     {
         uint64_t *s0 = (uint64_t *)st[0].seen;
         for (int t = 1; t < nt; ++t) {
@@ -228,6 +281,7 @@ static size_t encode_chip(int32_t n_pix, int32_t n_obs, const int16_t *spectra, 
     }
     h[0] = 1;
     h[3] = npal;
+    *(uint32_t *)(sec + 80) = drop;  /* the decoder's keep test */
     uint16_t *pal = (uint16_t *)(sec + 16);
     for (int j = 0; j < npal; ++j) {
         pal[j] = palv[j];
@@ -251,17 +305,17 @@ static size_t encode_chip(int32_t n_pix, int32_t n_obs, const int16_t *spectra, 
     /* pass 2: 4-bit QA codes and the kept band values (and the fill observations' values checked) */
 #pragma omp parallel num_threads(nt) reduction(| : bad2)
     {
-        uint8_t *keep = (uint8_t *)malloc((size_t)n_obs + 64);
-        uint32_t *km = (uint32_t *)malloc(((size_t)n_obs / 32 + 2) * 4);
+        uint8_t *keep = (uint8_t *)malloc(2 * (size_t)n_obs + 64), *strictm = keep + n_obs + 32;
+        uint32_t *km = (uint32_t *)malloc(((size_t)n_obs / 32 + 2) * 8), *sm = km + (n_obs / 32 + 2);
 #pragma omp for schedule(static)
         for (int32_t p = 0; p < n_pix; ++p) {
             const uint16_t *q = qa + (size_t)p * n_obs;
             uint8_t *r = q4 + (size_t)p * rowb;
 #if defined(__x86_64__)
             if (vec) {
-                qa_codes_avx512(q, n_obs, pal, npal, r, km);
+                qa_codes_avx512(q, n_obs, pal, npal, drop, strict, r, km, sm);
                 for (int b = 0; b < 7; ++b)
-                    compact_vbmi2(spectra + (size_t)b * plane + (size_t)p * n_obs, km, n_obs,
+                    compact_vbmi2(spectra + (size_t)b * plane + (size_t)p * n_obs, km, sm, n_obs,
                                   bands + (size_t)b * bstride + koff[p], &bad2);
                 continue;
             }
@@ -271,33 +325,38 @@ static size_t encode_chip(int32_t n_pix, int32_t n_obs, const int16_t *spectra, 
             for (; i + 1 < n_obs; i += 2) {
                 const uint16_t v0 = q[i], v1 = q[i + 1];
                 r[i >> 1] = (uint8_t)(lut[v0] | (lut[v1] << 4));
-                const uint32_t k0 = !(v0 & 1u), k1 = !(v1 & 1u);
+                const uint32_t k0 = !(v0 & drop), k1 = !(v1 & drop);
                 keep[i] = (uint8_t)k0;
                 keep[i + 1] = (uint8_t)k1;
+                strictm[i] = (uint8_t)((v0 & strict) != 0);
+                strictm[i + 1] = (uint8_t)((v1 & strict) != 0);
                 km[i >> 5] |= (k0 | (k1 << 1)) << (i & 31);
             }
             if (i < n_obs) {
                 const uint16_t v0 = q[i];
                 r[i >> 1] = lut[v0];
-                const uint32_t k0 = !(v0 & 1u);
+                const uint32_t k0 = !(v0 & drop);
                 keep[i] = (uint8_t)k0;
+                strictm[i] = (uint8_t)((v0 & strict) != 0);
                 km[i >> 5] |= k0 << (i & 31);
             }
             for (int b = 0; b < 7; ++b)
-                compact_scalar(spectra + (size_t)b * plane + (size_t)p * n_obs, keep, n_obs,
+                compact_scalar(spectra + (size_t)b * plane + (size_t)p * n_obs, keep, strictm, n_obs,
                                bands + (size_t)b * bstride + koff[p], &bad2);
         }
         free(keep);
         free(km);
     }
     free(lut);
-    if (bad2) return encode_raw(n_pix, n_obs, spectra, qa, sec, nt);  /* a fill observation with data */
+    if (bad2) return encode_raw(n_pix, n_obs, spectra, qa, sec, nt);  /* a strict observation with data */
     return sec_mode1(n_pix, n_obs, (int64_t)tot);
 }
 
 int64_t ccdgpu_encode_chips(int32_t n_chips, const int32_t *n_pix, const int32_t *n_obs, const int16_t *const *spectra,
-                            const uint16_t *const *qa, uint8_t *out, int64_t out_cap, int32_t threads) {
+                            const uint16_t *const *qa, uint8_t *out, int64_t out_cap, int32_t threads,
+                            uint16_t drop_bits, uint16_t strict_bits) {
     if (n_chips <= 0 || !n_pix || !n_obs || !spectra || !qa || !out) return -1;
+    if ((strict_bits & ~drop_bits) != 0) return -1;  /* a strict observation is a dropped one */
     const int64_t need = ccdgpu_encoded_bound(n_chips, n_pix, n_obs);
     if (need < 0 || out_cap < need) return -2;
     int64_t *tab = (int64_t *)out;
@@ -315,7 +374,8 @@ int64_t ccdgpu_encode_chips(int32_t n_chips, const int32_t *n_pix, const int32_t
     for (int32_t c = 0; c < n_chips; ++c) {
         off[c] = (int64_t)pos;
         pix[c] = pbase;
-        const size_t sz = encode_chip(n_pix[c], n_obs[c], spectra[c], qa[c], pbase, dbase, out + pos, threads, kept);
+        const size_t sz = encode_chip(n_pix[c], n_obs[c], spectra[c], qa[c], pbase, dbase, out + pos, threads, kept,
+                                      drop_bits, strict_bits);
         if (!sz) {
             free(kept);
             return -3;

@@ -102,10 +102,10 @@ __global__ __launch_bounds__(256) void ccd_unpack_b64(const unsigned char *__res
 }
 
 // ---- transport-encoded batches (ccd_encode.c; layout in include/ccdgpu.h) -> the standard
-// band-major spectra [7][n_pix][n_obs] and QA [n_pix][n_obs] of every chip, bit for bit.  One
-// wave per pixel, lane = observation: the 4-bit QA code through the chip's palette, the kept
-// (non-fill) observations' rank by ballot / mbcnt, band values gathered from the compacted
-// band columns (consecutive ranks: coalesced) and -9999 written for fill observations.  Byte
+// band-major spectra [7][n_pix][n_obs] and QA [n_pix][n_obs] of every chip.  One wave per
+// pixel, lane = observation: the 4-bit QA code through the chip's palette, the kept
+// observations' (no drop bit) rank by ballot / mbcnt, band values gathered from the compacted
+// band columns (consecutive ranks: coalesced) and -9999 written for the dropped ones.  Byte
 // work at HBM speed: ~13 B read and 16 B written per observation.
 constexpr int ENC_HDR = 128;
 __device__ __forceinline__ int64_t up16(int64_t x) { return (x + 15) & ~(int64_t)15; }
@@ -144,6 +144,7 @@ __global__ __launch_bounds__(256) void ccd_decode_enc(const unsigned char *__res
         return;
     }
     const uint16_t *pal = reinterpret_cast<const uint16_t *>(sec + 16);
+    const unsigned drop = *reinterpret_cast<const uint32_t *>(sec + 80);  // QA bits whose bands were not sent
     const uint32_t *koff = reinterpret_cast<const uint32_t *>(sec + ENC_HDR);
     const unsigned char *q4 = sec + ENC_HDR + up16(4 * ((int64_t)n_pix + 1));
     const int64_t rowb = (n_obs + 1) / 2;
@@ -155,7 +156,7 @@ __global__ __launch_bounds__(256) void ccd_decode_enc(const unsigned char *__res
         const bool in = i < n_obs;
         const unsigned code = in ? (qr[i >> 1] >> ((i & 1) * 4)) & 15u : 0u;
         const uint16_t q = pal[code];
-        const bool keep = in && !(q & 1u);
+        const bool keep = in && !(q & drop);
         const unsigned long long km = __ballot(keep);
         const int rank = carry + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(km >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)km, 0));
         if (in) {

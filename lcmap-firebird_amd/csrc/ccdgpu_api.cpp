@@ -171,6 +171,10 @@ struct ccdgpu_ctx {
     const int16_t *in_spectra = nullptr;
     const uint16_t *in_qa = nullptr;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // the host waits for a detection through this event: blocking (the waiting thread sleeps on
+    // the completion interrupt instead of polling), so the tile driver's waiting workers leave the
+    // host's CPUs to its fetch / encode threads
+    hipEvent_t done = nullptr;
     // staged batch
     bool staged = false, ran = false;
     ccdgpu_params params{};
@@ -236,6 +240,7 @@ struct ccdgpu_ctx {
         h_rows.release();
         for (auto &e : ev)
             if (e) (void)hipEventDestroy(e);
+        if (done) (void)hipEventDestroy(done);
         if (stream) (void)hipStreamDestroy(stream);
         release_arg_slot(arg_slot);
     }
@@ -344,6 +349,7 @@ int ccdgpu_init(int device, ccdgpu_ctx **out) {
         return fail(CCDGPU_EHIP, "hipStreamCreate failed");
     }
     for (auto &e : c->ev) (void)hipEventCreate(&e);
+    (void)hipEventCreateWithFlags(&c->done, hipEventBlockingSync | hipEventDisableTiming);
     if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return fail(CCDGPU_EHIP, "hipStreamCreate failed");
@@ -702,6 +708,10 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         if (ccdk_detect(c->n_slots, c->variant, sh.n_obs_max, c->arg_slot, c->stream))
             return fail(CCDGPU_EHIP, std::string("detect launch: ") + hipGetErrorString(hipGetLastError()));
         HIPCHK(hipEventRecord(c->ev[2], c->stream));
+        if (c->done) {  // sleep until the detection is done (the counters copy below is then quick)
+            HIPCHK(hipEventRecord(c->done, c->stream));
+            HIPCHK(hipEventSynchronize(c->done));
+        }
         unsigned long long h[8];
         HIPCHK(hipMemcpyAsync(h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));

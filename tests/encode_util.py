@@ -38,7 +38,8 @@ def decode(buf):
         qa = pal[codes[:, :n_obs]]
         b0 = q0 + up(n_pix * rowb, 16)
         bands = sec[b0:b0 + 14 * bstride].view(np.int16).reshape(7, bstride)
-        keep = (qa & 1) == 0
+        drop = int(sec[80:84].view(np.uint32)[0])
+        keep = (qa & drop) == 0
         assert int(keep.sum()) == kept == int(koff[-1])
         sp = np.full((7, n_pix, n_obs), -9999, dtype=np.int16)
         sp[:, keep] = bands[:, :kept]  # row-major boolean indexing = pixel-major kept order

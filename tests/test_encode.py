@@ -20,8 +20,8 @@ from ccdgpu import synth  # noqa: E402
 from encode_util import decode  # noqa: E402
 
 
-def encode(chips, threads=3):
-    e = ccdgpu.EncodedBatch.encode(chips, threads=threads, pinned=False)
+def encode(chips, threads=3, drop=1, strict=1):
+    e = ccdgpu.EncodedBatch.encode(chips, threads=threads, pinned=False, drop_bits=drop, strict_bits=strict)
     return e, e.buf[:e.nbytes_encoded]
 
 
@@ -87,6 +87,23 @@ def test_vector_and_scalar_encoders_write_the_same_bytes():
     if outs['0'][0] == 0:
         pytest.skip('no AVX-512 VBMI2 on this CPU: only the scalar encoder ran')
     assert outs['0'][1:] == outs['1'][1:]
+
+
+def test_unread_observations_dropped_and_the_rest_kept():
+    """drop = fill | cloud | shadow bits: the observations of those classes come back as -9999,
+    every other one (clear, water, snow, any other word) bit for bit; QA words all kept."""
+    drop, strict = ccdgpu.unread_drop_bits(None)
+    assert (drop, strict) == ((1 << 0) | (1 << 5) | (1 << 3), 1)
+    cfg = synth.config(3)
+    chips = [synth.chip(cfg, c, 0, 200) for c in (0, 1)]
+    e, buf = encode(chips, drop=drop, strict=strict)
+    raw = sum(s.nbytes + q.nbytes for _, s, q in chips)
+    assert e.nbytes_encoded < 0.6 * raw
+    for (d, s, q), (ds, dq) in zip(chips, decode(buf)):
+        np.testing.assert_array_equal(dq, q)
+        gone = (q & drop) != 0
+        np.testing.assert_array_equal(ds[:, ~gone], s[:, ~gone])
+        assert (ds[:, gone] == -9999).all()
 
 
 def test_encode_rejects_a_short_buffer():

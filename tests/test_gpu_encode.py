@@ -53,3 +53,41 @@ def test_encoded_upload_decodes_to_the_raw_inputs_and_detects_the_same():
     for a, b in zip(r0, r1):
         assert a.segments.tobytes() == b.segments.tobytes()
         assert np.array_equal(a.procedure, b.procedure) and np.array_equal(a.mask, b.mask)
+
+
+def test_unread_drop_encoding_detects_the_same():
+    """The runner's default encoding drops the band values of fill / cloud / shadow observations
+    (never read by any procedure): the device gets -9999 there and the raw values elsewhere, and
+    the detection -- segments, procedures, masks -- is the same as from the raw upload."""
+    import ccdgpu
+    from ccdgpu import synth
+    cs = [synth.chip(synth.config(3), 5, 0, 300), synth.chip(synth.config(5), 6, 0, 200),
+          synth.chip(synth.config(4), 7, 0, 200), synth.chip(synth.config(2), 8, 0, 150)]
+    drop, strict = ccdgpu.unread_drop_bits(None)
+    raw = ccdgpu.ChipBatch.from_chips(cs, pinned=True)
+    enc = ccdgpu.EncodedBatch.encode(cs, threads=4, drop_bits=drop, strict_bits=strict)
+    assert enc.nbytes_encoded < 0.65 * (raw.spectra.nbytes + raw.qa.nbytes)
+    ctx = ccdgpu.Context(0)
+    try:
+        ctx.stage_slot_chips(0, raw)
+        ctx.run_slot(0)
+        r0 = [ctx.fetch(c) for c in range(len(cs))]
+        ctx.stage_slot_encoded(1, enc)
+        ctx.run_slot(1)
+        s1, q1 = ctx.staged_inputs()
+        r1 = [ctx.fetch(c) for c in range(len(cs))]
+    finally:
+        ctx.close()
+    np.testing.assert_array_equal(q1, np.asarray(raw.qa))
+    gone = (np.asarray(raw.qa) & drop) != 0
+    s_raw = np.asarray(raw.spectra).reshape(-1)
+    for c in range(len(cs)):
+        d0, d1 = int(raw.data_off[c]), int(raw.data_off[c + 1])
+        sr = s_raw[7 * d0:7 * d1].reshape(7, -1)
+        se = s1[7 * d0:7 * d1].reshape(7, -1)
+        g = gone[d0:d1]
+        np.testing.assert_array_equal(se[:, ~g], sr[:, ~g])
+        assert (se[:, g] == -9999).all()
+    for a, b in zip(r0, r1):
+        assert a.segments.tobytes() == b.segments.tobytes()
+        assert np.array_equal(a.procedure, b.procedure) and np.array_equal(a.mask, b.mask)
