@@ -80,6 +80,8 @@ def parse():
     ap.add_argument('--tile-no-numa', action='store_true', help='tile leg: leave host threads unbound (A/B)')
     ap.add_argument('--tile-no-encode', action='store_true',
                     help='tile leg: upload raw chips (pool copies into pinned batches) instead of the transport encoding (A/B)')
+    ap.add_argument('--no-tile-lossless', action='store_true',
+                    help='skip the second tile run with the lossless encoding (reported as tile_lossless)')
     ap.add_argument('--tile-encode', choices=('unread', 'lossless'), default='unread',
                     help='tile leg transport encoding: drop the band values of fill/cloud/shadow observations '
                          '(never read by the detection; default) or only of fill observations (lossless)')
@@ -201,6 +203,13 @@ def main():
             dist.destroy_process_group()
         return
     tl = tile_leg(args, cfg, rank, world, device, dist)
+    tl_lossless = None
+    if not args.no_tile_lossless and not args.tile_no_encode and args.tile_encode != 'lossless':
+        # the same tile with the lossless encoding (device inputs bit-identical to the raw chips)
+        import copy
+        a2 = copy.copy(args)
+        a2.tile_encode = 'lossless'
+        tl_lossless = tile_leg(a2, cfg, rank, world, device, dist)
     if rank == 0:
         out = {
             'metric': 'pixels/sec change-detected (CONUS ARD tile) at 1/2/4/8 MI355X; FP64 VALU %',
@@ -217,12 +226,15 @@ def main():
             'data': 'synthetic (Landsat 4-8 ARD, seeded; tile leg: every chip distinct -- date-shifted copies of GPU-generated pool chips)',
             'config': {
                 'workload': '%s; one full 5000x5000-pixel tile per GPU (%d distinct 100x100-pixel chips per rank, %s), '
-                            'PCIe-inclusive: chips uploaded from pinned host memory (lossless transport encoding unless '
-                            '--tile-no-encode), detected, segment/pixel rows packed '
+                            'PCIe-inclusive: chips uploaded from pinned host memory in the runner\'s transport encoding '
+                            '(%s), detected, segment/pixel rows packed '
                             'on the device and fetched back, per-chip summaries gathered on rank 0 (ccdc.runner.changedetection); '
                             'a step = %d chips per rank' % (
                                 CONFIG_NAMES[args.config], tl['chips_per_rank'],
                                 ', '.join('%d chips of %d obs' % (v, k) for k, v in sorted(tl['n_obs_mix'].items())),
+                                'raw upload' if args.tile_no_encode else
+                                'band values of fill/cloud/shadow observations, which the detection never reads, not sent'
+                                if args.tile_encode == 'unread' else 'lossless',
                                 tl['chips_per_step']),
                 'workload_key': 'tile%d_config%d_chips%d_pcie' % (args.tile_chips, args.config, tl['chips_per_rank']),
                 'synthetic_config': args.config,
@@ -238,6 +250,9 @@ def main():
             'resident': res,
             'tile': tl,
         }
+        if tl_lossless is not None:
+            out['tile_lossless'] = {k: tl_lossless[k] for k in ('value', 'unit', 'seconds', 'transport_encoding',
+                                                                 'worker_seconds_rank0')}
         if not args.no_packer:
             ctx = ccdgpu.Context(device)
             out['chip_packer'] = packer_leg(ctx, res['batch'])
