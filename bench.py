@@ -75,8 +75,8 @@ def parse():
                     help='resident leg only (kernel A/B runs): value = the resident rate, not the headline metric')
     ap.add_argument('--tile-batch', type=int, default=8, help='chips per launch in the tile leg')
     ap.add_argument('--tile-pool', type=int, default=32, help='generated chips behind the tile leg\'s chips (each position a date-shifted copy)')
-    ap.add_argument('--tile-contexts', type=int, default=3, help='contexts per GPU in the tile leg')
-    ap.add_argument('--tile-copy-threads', type=int, default=4, help='host threads per pool-chip copy in the tile leg source (3 contexts x 4 within the box\'s 16-CPU quota)')
+    ap.add_argument('--tile-contexts', type=int, default=4, help='contexts per GPU in the tile leg')
+    ap.add_argument('--tile-copy-threads', type=int, default=3, help='host threads per batch encode (or pool-chip copy) in the tile leg source (4 contexts x 3 within the box\'s 16-CPU quota)')
     ap.add_argument('--tile-no-numa', action='store_true', help='tile leg: leave host threads unbound (A/B)')
     ap.add_argument('--tile-no-encode', action='store_true',
                     help='tile leg: upload raw chips (pool copies into pinned batches) instead of the transport encoding (A/B)')

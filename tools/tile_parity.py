@@ -135,6 +135,7 @@ def main():
     ap.add_argument('--batch', type=int, default=8)
     ap.add_argument('--oracle-threads', type=int, default=int(os.environ.get('OMP_NUM_THREADS', '16') or 16) - 1)
     ap.add_argument('--out', default=os.path.join(ROOT, 'gpurun_out', 'tile_parity.json'))
+    ap.add_argument('--encode', choices=('unread', 'lossless', 'none'), default='unread', help='upload of the chips (the runner\'s default: unread)')
     ap.add_argument('--cpu-dry-run', action='store_true',
                     help='plumbing check without a GPU: host generator, oracle-backed contexts (tests/rows_util)')
     args = ap.parse_args()
@@ -159,8 +160,9 @@ def main():
     sink = SampleSink(args.sample)
     xys = [(-1815585 + 3000 * (c // 50), 1064805 - 3000 * (c % 50)) for c in range(args.chips)]
     t = time.perf_counter()
+    enc = {'unread': True, 'lossless': 'lossless', 'none': False}[args.encode]
     res = runner.changedetection(xys, src, contexts=2, batch_chips=args.batch, sink=sink, upload_depth=2,
-                                 context_factory=factory)
+                                 context_factory=factory, encode=enc)
     gpu_s = time.perf_counter() - t
     print('tile of %d chips detected in %.1f s; waiting for the oracle' % (args.chips, gpu_s), flush=True)
     tot = {'pixels': 0, 'segments': 0, 'int_mismatches': 0, 'mask_mismatches': 0, 'float_mismatches': 0}
@@ -198,6 +200,8 @@ def main():
         'chips_with_mismatches': bad_chips[:50], 'first_mismatches': notes[:20],
         'detect_seconds': gpu_s, 'total_seconds': total_s, 'generate_seconds': src.generate_seconds,
         'oracle_threads': args.oracle_threads,
+        'upload': {'unread': 'transport encoding, unread setting (band values of fill/cloud/shadow observations not sent)',
+                   'lossless': 'transport encoding, lossless setting', 'none': 'raw'}[args.encode],
         'compare': 'rows and mask words: row count, sday/eday/bday, curqa, has_model, chprob, processing mask bit-exact; '
                    'mag/rmse/intercept/coef within 1e-6 relative + 2 float32 ulp of the oracle rows',
         'chip_digests_sha1': __import__('hashlib').sha1(''.join(c['digest'] for c in res['chips']).encode()).hexdigest(),
