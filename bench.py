@@ -387,6 +387,16 @@ def max_over_ranks(x, dist):
     return float(t.item())
 
 
+def _cgroup_cpu():
+    """The process cgroup's CPU accounting (cgroup v2 cpu.stat: usage and throttling, usec), or
+    None: whether the box's CPU quota throttled the host side of a timed run."""
+    try:
+        with open('/sys/fs/cgroup/cpu.stat') as f:
+            return {k: int(v) for k, v in (ln.split() for ln in f if ln.strip())}
+    except (OSError, ValueError):
+        return None
+
+
 class _Offset(object):
     """A source whose positions are shifted by ``off`` (the warmup's chips: another tile range)."""
 
@@ -492,6 +502,7 @@ def tile_leg(args, cfg, rank, world, device, dist):
     ctxs[0].synchronize()
     gen0 = src.generate_seconds
     enc0 = (esrc.bytes_raw, esrc.bytes_sent, esrc.encode_seconds) if encode else (0, 0, 0.0)
+    cg0 = _cgroup_cpu()
     t = time.perf_counter()
     res = run(total, src_timed)
     ctxs[0].synchronize()
@@ -499,6 +510,11 @@ def tile_leg(args, cfg, rank, world, device, dist):
         dist.barrier()
     el = max_over_ranks(time.perf_counter() - t, dist)
     gen_s = src.generate_seconds - gen0
+    cg1 = _cgroup_cpu()
+    cg = None
+    if cg0 and cg1:
+        cg = {k.replace('_usec', '_s'): round((cg1[k] - cg0[k]) / 1e6, 3) for k in cg0 if k in cg1 and k.endswith('usec')}
+        cg.update({k: cg1[k] - cg0[k] for k in cg0 if k in cg1 and not k.endswith('usec')})
     enc_stats = None
     if encode:
         raw_b, sent_b = esrc.bytes_raw - enc0[0], esrc.bytes_sent - enc0[1]
@@ -528,6 +544,7 @@ def tile_leg(args, cfg, rank, world, device, dist):
             'source_copy_threads': args.tile_copy_threads if mode == 'pool' else None,
             'gpu_numa_node': numa_node, 'host_threads_bound_to_gpu_node': not args.tile_no_numa,
             'transport_encoding': enc_stats,
+            'cgroup_cpu_during_tile_s': cg,
             'source_prepare_seconds': round(prep_s, 2),
             'generate_seconds_rank0': round(gen_s, 3),
             'pinned_pool_batches': src.allocated,

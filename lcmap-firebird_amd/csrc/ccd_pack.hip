@@ -143,7 +143,9 @@ __global__ __launch_bounds__(256) void ccd_decode_enc(const unsigned char *__res
         }
         return;
     }
-    const uint16_t *pal = reinterpret_cast<const uint16_t *>(sec + 16);
+    // the palette in registers (lane j < 16 holds entry j): a code is looked up with one lane
+    // permute instead of a dependent global load
+    const uint16_t palr = l < 16 ? reinterpret_cast<const uint16_t *>(sec + 16)[l] : (uint16_t)0;
     const unsigned drop = *reinterpret_cast<const uint32_t *>(sec + 80);  // QA bits whose bands were not sent
     const uint32_t *koff = reinterpret_cast<const uint32_t *>(sec + ENC_HDR);
     const unsigned char *q4 = sec + ENC_HDR + up16(4 * ((int64_t)n_pix + 1));
@@ -151,27 +153,49 @@ __global__ __launch_bounds__(256) void ccd_decode_enc(const unsigned char *__res
     const int16_t *bands = reinterpret_cast<const int16_t *>(q4 + up16((int64_t)n_pix * rowb)) + koff[p];
     const unsigned char *qr = q4 + p * rowb;
     int carry = 0;
-    for (int i0 = 0; i0 < n_obs; i0 += 64) {
-        const int i = i0 + l;
-        const bool in = i < n_obs;
-        const unsigned code = in ? (qr[i >> 1] >> ((i & 1) * 4)) & 15u : 0u;
-        const uint16_t q = pal[code];
-        const bool keep = in && !(q & drop);
-        const unsigned long long km = __ballot(keep);
-        const int rank = carry + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(km >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)km, 0));
-        if (in) {
-            qo[i] = q;
-            int16_t v[7];
+    // four 64-observation chunks per round: their code bytes load together, then their ranks,
+    // then all 28 band loads go out before the first store (latency once per round, not per chunk)
+    constexpr int U = 4;
+    for (int i0 = 0; i0 < n_obs; i0 += U * 64) {
+        unsigned cb[U];
 #pragma unroll
-            for (int b = 0; b < 7; ++b) v[b] = (int16_t)-9999;
-            if (keep) {  // (loads under the lane's own mask: a fill lane's rank may point past the column)
-#pragma unroll
-                for (int b = 0; b < 7; ++b) v[b] = bands[b * bstride + rank];
-            }
-#pragma unroll
-            for (int b = 0; b < 7; ++b) sp[(int64_t)b * plane + i] = v[b];
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * 64 + l;
+            cb[u] = i < n_obs ? (unsigned)qr[i >> 1] : 0u;
         }
-        carry += __popcll(km);
+        uint16_t q[U];
+        bool keep[U];
+        int rank[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * 64 + l;
+            const bool in = i < n_obs;
+            const int code = (int)((cb[u] >> ((i & 1) * 4)) & 15u);
+            q[u] = (uint16_t)__shfl((int)palr, code, 64);
+            keep[u] = in && !(q[u] & drop);
+            const unsigned long long km = __ballot(keep[u]);
+            rank[u] = carry + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(km >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)km, 0));
+            carry += __popcll(km);
+        }
+        int16_t v[U][7];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+            for (int b = 0; b < 7; ++b) v[u][b] = (int16_t)-9999;
+            if (keep[u]) {  // (loads under the lane's own mask: a dropped lane's rank may point past the column)
+#pragma unroll
+                for (int b = 0; b < 7; ++b) v[u][b] = bands[b * bstride + rank[u]];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * 64 + l;
+            if (i < n_obs) {
+                qo[i] = q[u];
+#pragma unroll
+                for (int b = 0; b < 7; ++b) sp[(int64_t)b * plane + i] = v[u][b];
+            }
+        }
     }
 }
 

@@ -199,6 +199,11 @@ struct ccdgpu_ctx {
     DevBuf<int32_t> row_xy;     // per-chip (cx, cy) of a batch row fetch
     DevBuf<int8_t> mask8;
     PinBuf h_rows;              // pinned landing zone of a batch row fetch (rows, then mask words)
+    // pinned staging of every launch's small host <-> device copies (initial counters, kernel
+    // arguments, counters and statistics read back, CSR offsets): DMA from / to pinned memory,
+    // where pageable memory would go through a runtime staging copy -- a blit kernel that has to
+    // wait for free CUs while other contexts' detection kernels hold them all
+    PinBuf h_small, h_off;
     DevBuf<int64_t> slot_dates[CCDGPU_UPLOAD_SLOTS];   // upload slots (ccdgpu_stage_slot / ccdgpu_run_slot)
     DevBuf<int16_t> slot_spectra[CCDGPU_UPLOAD_SLOTS];
     DevBuf<uint16_t> slot_qa[CCDGPU_UPLOAD_SLOTS];
@@ -238,6 +243,8 @@ struct ccdgpu_ctx {
         rows.release();
         mask8.release();
         h_rows.release();
+        h_small.release();
+        h_off.release();
         for (auto &e : ev)
             if (e) (void)hipEventDestroy(e);
         if (done) (void)hipEventDestroy(done);
@@ -344,13 +351,33 @@ int ccdgpu_init(int device, ccdgpu_ctx **out) {
         return fail(CCDGPU_EHIP, "device " + std::to_string(device) + " is " + arch + ", libccdgpu is built for gfx950 only");
     }
     c->n_cu = prop.multiProcessorCount;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    // CCDGPU_COPY_CUS = k > 0: the copy stream (uploads' decode kernel, blits) gets k CUs of its
+    // own -- the same k for every context -- and the detection stream the rest, so a context's
+    // upload is never starved of CUs by other contexts' persistent detection waves (which
+    // otherwise hold every wave slot until their launch drains).  Reserved: the last k / 8 CUs of
+    // each group of n_cu / 8 (one group per XCD, if the mask numbers CUs XCD-major).
+    int copy_cus = 0;
+    if (const char *e = std::getenv("CCDGPU_COPY_CUS")) copy_cus = std::atoi(e);
+    std::vector<uint32_t> mask_det, mask_copy;
+    if (copy_cus > 0 && copy_cus < c->n_cu) {
+        const int nw = (c->n_cu + 31) / 32, groups = 8, per = c->n_cu / groups, k = (copy_cus + groups - 1) / groups;
+        mask_det.assign(nw, 0u);
+        mask_copy.assign(nw, 0u);
+        for (int cu = 0; cu < c->n_cu; ++cu) {
+            const bool reserved = per > k && (cu % per) >= per - k;
+            (reserved ? mask_copy : mask_det)[cu / 32] |= 1u << (cu % 32);
+        }
+    }
+    const bool masked = !mask_det.empty();
+    if ((masked ? hipExtStreamCreateWithCUMask(&c->stream, (uint32_t)mask_det.size(), mask_det.data())
+                : hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
         delete c;
         return fail(CCDGPU_EHIP, "hipStreamCreate failed");
     }
     for (auto &e : c->ev) (void)hipEventCreate(&e);
     (void)hipEventCreateWithFlags(&c->done, hipEventBlockingSync | hipEventDisableTiming);
-    if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) {
+    if ((masked ? hipExtStreamCreateWithCUMask(&c->copy_stream, (uint32_t)mask_copy.size(), mask_copy.data())
+                : hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking)) != hipSuccess) {
         delete c;
         return fail(CCDGPU_EHIP, "hipStreamCreate failed");
     }
@@ -696,10 +723,18 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         a.pool = c->pool.p;
         a.pool_seq = c->pool_seq.p;
         a.pool_cap = c->pool_cap;
-        unsigned long long init[8] = {0ull, 0ull, ~0ull, 0ull, 0ull, ~0ull, 0ull, ~0ull};
-        HIPCHK(hipMemcpyAsync(c->counters.p, init, sizeof(init), hipMemcpyHostToDevice, c->stream));
+        // h_small: [0, 64) initial counters, [64, 128) counters back, [128, 128 + 8 NSTATS) stats
+        // back, then the kernel arguments (each launch waits for the previous one's copies)
+        constexpr size_t SM_ARGS = 128 + 8 * CCD_NSTATS;
+        if (int rc0 = c->h_small.ensure(SM_ARGS + sizeof(CcdDetectArgs))) return rc0;
+        unsigned long long *hinit = reinterpret_cast<unsigned long long *>(c->h_small.p);
+        const unsigned long long init[8] = {0ull, 0ull, ~0ull, 0ull, 0ull, ~0ull, 0ull, ~0ull};
+        std::memcpy(hinit, init, sizeof(init));
+        HIPCHK(hipMemcpyAsync(c->counters.p, hinit, sizeof(init), hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipMemsetAsync(c->stats.p, 0, sizeof(unsigned long long) * CCD_NSTATS, c->stream));
-        if (ccdk_set_args(&a, c->arg_slot, c->stream)) return fail(CCDGPU_EHIP, "copying kernel arguments to constant memory failed");
+        CcdDetectArgs *hargs = reinterpret_cast<CcdDetectArgs *>(c->h_small.p + SM_ARGS);
+        std::memcpy(hargs, &a, sizeof(a));
+        if (ccdk_set_args(hargs, c->arg_slot, c->stream)) return fail(CCDGPU_EHIP, "copying kernel arguments to constant memory failed");
         HIPCHK(hipEventRecord(c->ev[0], c->stream));
         if (ccdk_prep(c->in_dates, nc, c->chip_nobs.p, c->chip_obs_off.p, p.avg_days_yr, c->order.p, c->sdates.p, c->basis.p,
                       c->stream))
@@ -708,18 +743,21 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         if (ccdk_detect(c->n_slots, c->variant, sh.n_obs_max, c->arg_slot, c->stream))
             return fail(CCDGPU_EHIP, std::string("detect launch: ") + hipGetErrorString(hipGetLastError()));
         HIPCHK(hipEventRecord(c->ev[2], c->stream));
-        if (c->done) {  // sleep until the detection is done (the counters copy below is then quick)
+        // counters and statistics back into pinned memory, then sleep until they have landed
+        unsigned long long *h = reinterpret_cast<unsigned long long *>(c->h_small.p + 64);
+        unsigned long long *hst = reinterpret_cast<unsigned long long *>(c->h_small.p + 128);
+        HIPCHK(hipMemcpyAsync(h, c->counters.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(hst, c->stats.p, sizeof(unsigned long long) * CCD_NSTATS, hipMemcpyDeviceToHost, c->stream));
+        if (c->done) {
             HIPCHK(hipEventRecord(c->done, c->stream));
             HIPCHK(hipEventSynchronize(c->done));
+        } else {
+            HIPCHK(hipStreamSynchronize(c->stream));
         }
-        unsigned long long h[8];
-        HIPCHK(hipMemcpyAsync(h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
         if (h[4] >= 100000) {
             // checking build: every call site that ran without a full EXEC, from the line bitmap
             // (bit = line / 2) in stats[8 ..]
-            unsigned long long st[CCD_NSTATS];
-            HIPCHK(hipMemcpy(st, c->stats.p, sizeof(st), hipMemcpyDeviceToHost));
+            const unsigned long long *st = hst;
             std::string lines;
             for (int w = 8; w < CCD_NSTATS; ++w)
                 for (int b = 0; b < 64; ++b)
@@ -741,8 +779,7 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         float ms_prep = 0.f, ms_det = 0.f;
         (void)hipEventElapsedTime(&ms_prep, c->ev[0], c->ev[1]);
         (void)hipEventElapsedTime(&ms_det, c->ev[1], c->ev[2]);
-        unsigned long long st[CCD_NSTATS];
-        HIPCHK(hipMemcpy(st, c->stats.p, sizeof(st), hipMemcpyDeviceToHost));
+        const unsigned long long *st = hst;
         for (int i = 0; i < CCD_NSTATS; ++i) c->diag[i] = st[i];
         // CSR: exclusive scan of per-pixel counts, then scatter the pool
         int rc;
@@ -753,8 +790,10 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         // nseg has total_pix entries; the scan over total_pix+1 needs a trailing zero
         HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->cub_tmp.p, tmp_bytes, c->nseg.p, c->offsets.p, (int)c->total_pix, c->stream));
         c->h_offsets.resize(c->total_pix + 1);
-        HIPCHK(hipMemcpyAsync(c->h_offsets.data(), c->offsets.p, sizeof(int64_t) * c->total_pix, hipMemcpyDeviceToHost, c->stream));
+        if ((rc = c->h_off.ensure(sizeof(int64_t) * (size_t)c->total_pix))) return rc;
+        HIPCHK(hipMemcpyAsync(c->h_off.p, c->offsets.p, sizeof(int64_t) * c->total_pix, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
+        std::memcpy(c->h_offsets.data(), c->h_off.p, sizeof(int64_t) * (size_t)c->total_pix);
         c->h_offsets[c->total_pix] = c->n_pool;
         if (ccdk_scatter(c->pool.p, c->pool_seq.p, c->n_pool, c->offsets.p, c->chip_pix_off.p, nc, c->csr.p, c->stream))
             return fail(CCDGPU_EHIP, "scatter launch failed");
