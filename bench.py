@@ -76,6 +76,7 @@ def parse():
     ap.add_argument('--tile-batch', type=int, default=8, help='chips per launch in the tile leg')
     ap.add_argument('--tile-pool', type=int, default=32, help='generated chips behind the tile leg\'s chips (each position a date-shifted copy)')
     ap.add_argument('--tile-contexts', type=int, default=4, help='contexts per GPU in the tile leg')
+    ap.add_argument('--tile-copy-cus', type=int, default=8, help='CUs each tile context reserves for its upload stream (ccdgpu_init_copy_cus; 0 = none)')
     ap.add_argument('--tile-copy-threads', type=int, default=3, help='host threads per batch encode (or pool-chip copy) in the tile leg source (4 contexts x 3 within the box\'s 16-CPU quota)')
     ap.add_argument('--tile-no-numa', action='store_true', help='tile leg: leave host threads unbound (A/B)')
     ap.add_argument('--tile-no-encode', action='store_true',
@@ -181,7 +182,7 @@ def main():
         if rank == 0:
             print(json.dumps({'metric': 'tile leg only (knob sweep)', 'value': tl['value'], 'unit': 'pixels/s',
                               'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': tl['ms_per_step'],
-                              'tile': tl, 'knobs': {'tile_batch': args.tile_batch, 'tile_contexts': args.tile_contexts,
+                              'tile': tl, 'knobs': {'tile_batch': args.tile_batch, 'tile_contexts': args.tile_contexts, 'tile_copy_cus': args.tile_copy_cus,
                                                     'tile_depth': args.tile_depth,
                                                     'HSA_ENABLE_SDMA': os.environ.get('HSA_ENABLE_SDMA')}}),
                   file=json_out, flush=True)
@@ -475,7 +476,7 @@ def tile_leg(args, cfg, rank, world, device, dist):
         src.prefill(n_inflight)
         src_timed = src_warm = src
     prep_s = time.perf_counter() - t_prep
-    ctxs = [ccdgpu.Context(device) for _ in range(args.tile_contexts)]
+    ctxs = [ccdgpu.Context(device, copy_cus=args.tile_copy_cus) for _ in range(args.tile_contexts)]
     lent = iter([])
 
     def factory(dev):

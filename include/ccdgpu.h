@@ -139,6 +139,16 @@ void ccdgpu_params_default(ccdgpu_params *p);
  * detections concurrently (each has its own stream, buffers and launch-argument slot), so a
  * second context's launch fills the CUs the first one's launch tail leaves idle. */
 int ccdgpu_init(int device, ccdgpu_ctx **ctx);
+/* ccdgpu_init with `copy_cus` CUs reserved for everything of the context but the detection kernel
+ * -- the encoded upload's decode kernel, the launch's prep, CSR scan and scatter, the row packing
+ * and the small copies -- and the rest for the detection kernel; 0 = no reservation
+ * (ccdgpu_init: all on one stream).  Persistent detection waves hold every wave slot of their
+ * CUs until the launch drains, so with several contexts one context's short kernels otherwise
+ * wait for wave slots behind the others' whole detections; the tile driver (ccdc.runner)
+ * reserves 8 of 256.  CCDGPU_COPY_CUS in the
+ * environment overrides the value.  (No reference counterpart: an execution detail of the
+ * pipelined driver that replaces ccdc/pyccd.py:168's per-chip map.) */
+int ccdgpu_init_copy_cus(int device, int copy_cus, ccdgpu_ctx **ctx);
 int ccdgpu_destroy(ccdgpu_ctx *ctx);
 int ccdgpu_device_count(int *count);
 /* NUMA node of HIP device `device`'s PCIe attachment (sysfs numa_node of its bus id; -1 when the

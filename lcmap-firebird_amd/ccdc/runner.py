@@ -398,7 +398,7 @@ def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, er
 
 def detect_tile(xys, source, queue, device=0, contexts=4, batch_chips=8, params=None, width=100,
                 sink=None, context_factory=None, upload_depth=2, tail_chips=None, bind_numa=True, encode=True,
-                encode_threads=3):
+                encode_threads=3, copy_cus=8):
     """Change detection of the tile chips at ``xys`` (list of (cx, cy), tile order) on one GPU.
 
     ``source(positions) -> ccdgpu.ChipBatch`` supplies the ARD of the chips at those tile
@@ -413,7 +413,9 @@ def detect_tile(xys, source, queue, device=0, contexts=4, batch_chips=8, params=
     full batches per context of this process).  ``encode``: upload every batch in the transport
     encoding (EncodingSource, ``encode_threads`` host threads per fetch; True = its 'unread'
     setting, 'lossless' = lossless) instead of raw -- ``source`` may then also be an
-    EncodingSource already (its counters are reported)."""
+    EncodingSource already (its counters are reported).  ``copy_cus``: CUs each context reserves
+    for its upload (decode kernel, blits) so other contexts' persistent detection waves cannot
+    starve it (ccdgpu_init_copy_cus; 0 = none; not used with a ``context_factory``)."""
     from ccdgpu import UPLOAD_SLOTS
     if not 1 <= int(upload_depth) <= UPLOAD_SLOTS - 1:
         raise ValueError('upload_depth must be in 1 .. %d (ccdgpu.UPLOAD_SLOTS - 1), got %r' % (UPLOAD_SLOTS - 1, upload_depth))
@@ -423,7 +425,9 @@ def detect_tile(xys, source, queue, device=0, contexts=4, batch_chips=8, params=
         tail_chips = 2 * int(batch_chips) * max(1, int(contexts))
     if context_factory is None:
         import ccdgpu
-        context_factory = ccdgpu.Context
+
+        def context_factory(dev):
+            return ccdgpu.Context(dev, copy_cus=copy_cus)
     if encode and not isinstance(source, EncodingSource):
         source = EncodingSource(source, threads=encode_threads, drop='lossless' if encode == 'lossless' else 'unread',
                                 params=params)
@@ -499,7 +503,7 @@ class TileError(RuntimeError):
 
 def changedetection(tile, source, device=None, contexts=4, batch_chips=8, number=None, params=None,
                     sink=None, width=100, context_factory=None, ctx=None, upload_depth=2, tail_chips=None,
-                    bind_numa=True, encode=True, encode_threads=3):
+                    bind_numa=True, encode=True, encode_threads=3, copy_cus=8):
     """Change detection for a tile on every GPU of the job (reference core.changedetection,
     ccdc/core.py:78-123).
 
@@ -542,7 +546,7 @@ def changedetection(tile, source, device=None, contexts=4, batch_chips=8, number
         sink, stats = detect_tile(xys, source, queue, device=device, contexts=contexts, batch_chips=batch_chips,
                                   params=params, width=width, sink=sink, context_factory=context_factory,
                                   upload_depth=upload_depth, tail_chips=tail_chips, bind_numa=bind_numa,
-                                  encode=encode, encode_threads=encode_threads)
+                                  encode=encode, encode_threads=encode_threads, copy_cus=copy_cus)
     except Exception as e:
         if not (dist_on and dist.get_world_size() > 1):
             raise

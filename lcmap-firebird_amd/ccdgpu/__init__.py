@@ -38,6 +38,9 @@ def _declare(L):
     L.ccdgpu_last_error.restype = c.c_char_p
     L.ccdgpu_params_default.argtypes = [c.POINTER(abi.Params)]
     L.ccdgpu_init.argtypes = [c.c_int, c.POINTER(c.c_void_p)]
+    if hasattr(L, 'ccdgpu_init_copy_cus'):
+        L.ccdgpu_init_copy_cus.argtypes = [c.c_int, c.c_int, c.POINTER(c.c_void_p)]
+        L.ccdgpu_init_copy_cus.restype = c.c_int
     L.ccdgpu_destroy.argtypes = [c.c_void_p]
     L.ccdgpu_device_count.argtypes = [c.POINTER(c.c_int)]
     if hasattr(L, 'ccdgpu_encode_chips'):  # (absent from libraries built before it: A/B runs)
@@ -96,7 +99,7 @@ EXPORTS = ('ccdgpu_version', 'ccdgpu_last_error', 'ccdgpu_params_default', 'ccdg
            'ccdgpu_host_alloc', 'ccdgpu_host_free', 'ccdgpu_stage_slot', 'ccdgpu_run_slot',
            'ccdgpu_last_stats', 'ccdgpu_diag_counters', 'ccdgpu_stage_chips', 'ccdgpu_stage_slot_chips',
            'ccdgpu_fetch_batch_rows', 'ccdgpu_device_numa_node', 'ccdgpu_encoded_bound', 'ccdgpu_encode_chips',
-           'ccdgpu_encode_vector_path', 'ccdgpu_stage_slot_encoded')
+           'ccdgpu_encode_vector_path', 'ccdgpu_stage_slot_encoded', 'ccdgpu_init_copy_cus')
 
 
 def lib():
@@ -354,10 +357,16 @@ def _as_inputs(dates, spectra, qa):
 class Context(object):
     """One HIP device + stream (ccdgpu_ctx).  Not shared across threads."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, copy_cus=0):
+        """copy_cus > 0 reserves that many CUs for the context's copy stream (upload decode,
+        blits), the rest for detection (ccdgpu_init_copy_cus, include/ccdgpu.h)."""
         self.qa_error = False
         self._ctx = ctypes.c_void_p()
-        _check(lib().ccdgpu_init(int(device), ctypes.byref(self._ctx)))
+        L = lib()
+        if copy_cus and hasattr(L, 'ccdgpu_init_copy_cus'):
+            _check(L.ccdgpu_init_copy_cus(int(device), int(copy_cus), ctypes.byref(self._ctx)))
+        else:
+            _check(L.ccdgpu_init(int(device), ctypes.byref(self._ctx)))
         self.device = device
 
     def close(self):

@@ -146,8 +146,9 @@ __attribute__((target("avx512f,avx512bw,avx512vl,avx512vbmi2"))) static uint32_t
         const __mmask32 lm = n - i >= 32 ? (__mmask32)0xFFFFFFFFu : (__mmask32)((1u << (n - i)) - 1u);
         const __m512i v = _mm512_maskz_loadu_epi16(lm, (const void *)(q + i));
         fill += (uint32_t)__builtin_popcount(_mm512_test_epi16_mask(v, one) & lm);
-        __mmask32 un = lm;
-        for (int j = 0; j < np && un; ++j) un &= ~_mm512_cmpeq_epi16_mask(v, _mm512_set1_epi16((short)s_pal[j]));
+        __mmask32 hit = 0;  /* independent compares (an early-exit chain measured 1.7x slower) */
+        for (int j = 0; j < np; ++j) hit |= _mm512_cmpeq_epi16_mask(v, _mm512_set1_epi16((short)s_pal[j]));
+        __mmask32 un = lm & ~hit;
         while (un) {
             const uint16_t w = q[i + __builtin_ctz(un)];
             if (np < 17) s_pal[np++] = w;
@@ -172,6 +173,18 @@ static int have_vbmi2(void) { return 0; }
 #endif
 
 int32_t ccdgpu_encode_vector_path(void) { return have_vbmi2(); }
+
+/* pixels per block of the vector pass 2 (CCDGPU_ENCODE_BLOCK overrides the default 32; 1 = the
+ * bands of one pixel after another) */
+static int enc_block(void) {
+    static int b = 0;
+    if (!b) {
+        const char *e = getenv("CCDGPU_ENCODE_BLOCK");
+        int v = e ? atoi(e) : 32;
+        b = v < 1 ? 1 : v > 256 ? 256 : v;
+    }
+    return b;
+}
 
 /* per-thread pass-1 state: the QA words seen (a 65536-bit set), a fill observation with a band
  * value other than -9999 */
@@ -302,24 +315,39 @@ static size_t encode_chip(int32_t n_pix, int32_t n_obs, const int16_t *spectra, 
     int16_t *bands = (int16_t *)(q4 + up((size_t)n_pix * rowb, 16));
     const int vec = have_vbmi2();
     int bad2 = 0;
-    /* pass 2: 4-bit QA codes and the kept band values (and the fill observations' values checked) */
+    /* pass 2: 4-bit QA codes and the kept band values (and the fill observations' values checked).
+     * Vector path in blocks of enc_block() pixels: the block's keep / strict masks first, then one
+     * band at a time over the whole block, so the loads and stores run as two long sequential
+     * streams (band rows of consecutive pixels are contiguous in the input plane and in the
+     * output) instead of seven of each interleaved per pixel. */
+    const int mw = n_obs / 32 + 2;  /* mask words per pixel */
+    const int pb = enc_block();
 #pragma omp parallel num_threads(nt) reduction(| : bad2)
     {
         uint8_t *keep = (uint8_t *)malloc(2 * (size_t)n_obs + 64), *strictm = keep + n_obs + 32;
-        uint32_t *km = (uint32_t *)malloc(((size_t)n_obs / 32 + 2) * 8), *sm = km + (n_obs / 32 + 2);
+        uint32_t *km = (uint32_t *)malloc((size_t)mw * 8 * pb), *sm = km + (size_t)mw * pb;
+#if defined(__x86_64__)
+        if (vec) {
+#pragma omp for schedule(static)
+            for (int32_t p0 = 0; p0 < n_pix; p0 += pb) {
+                const int32_t pe = p0 + pb < n_pix ? p0 + pb : n_pix;
+                for (int32_t p = p0; p < pe; ++p)
+                    qa_codes_avx512(qa + (size_t)p * n_obs, n_obs, pal, npal, drop, strict, q4 + (size_t)p * rowb,
+                                    km + (size_t)(p - p0) * mw, sm + (size_t)(p - p0) * mw);
+                for (int b = 0; b < 7; ++b) {
+                    const int16_t *src = spectra + (size_t)b * plane;
+                    int16_t *dst = bands + (size_t)b * bstride;
+                    for (int32_t p = p0; p < pe; ++p)
+                        compact_vbmi2(src + (size_t)p * n_obs, km + (size_t)(p - p0) * mw, sm + (size_t)(p - p0) * mw,
+                                      n_obs, dst + koff[p], &bad2);
+                }
+            }
+        } else
+#endif
 #pragma omp for schedule(static)
         for (int32_t p = 0; p < n_pix; ++p) {
             const uint16_t *q = qa + (size_t)p * n_obs;
             uint8_t *r = q4 + (size_t)p * rowb;
-#if defined(__x86_64__)
-            if (vec) {
-                qa_codes_avx512(q, n_obs, pal, npal, drop, strict, r, km, sm);
-                for (int b = 0; b < 7; ++b)
-                    compact_vbmi2(spectra + (size_t)b * plane + (size_t)p * n_obs, km, sm, n_obs,
-                                  bands + (size_t)b * bstride + koff[p], &bad2);
-                continue;
-            }
-#endif
             memset(km, 0, ((size_t)n_obs / 32 + 1) * 4);
             int32_t i = 0;
             for (; i + 1 < n_obs; i += 2) {

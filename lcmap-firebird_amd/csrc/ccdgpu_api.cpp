@@ -165,6 +165,12 @@ struct ccdgpu_ctx {
     int arg_slot = -1;  // this context's launch-argument slot in constant memory
     hipStream_t stream = nullptr;
     hipStream_t copy_stream = nullptr;  // uploads of ccdgpu_stage_slot (overlap a running detection)
+    // every other kernel and copy of a launch (prep, CSR scan and scatter, row packing, small
+    // copies): the detection stream itself, or -- with CUs reserved (ccdgpu_init_copy_cus) -- a
+    // stream on the reserved CUs, so these short kernels never wait for wave slots behind
+    // persistent detection waves; only the detection kernel then runs on `stream`
+    hipStream_t aux = nullptr;
+    bool aux_own = false;
     hipEvent_t uploaded[CCDGPU_UPLOAD_SLOTS] = {};
     // inputs the next detection reads: the single staged batch, or one of the two upload slots
     const int64_t *in_dates = nullptr;
@@ -203,7 +209,7 @@ struct ccdgpu_ctx {
     // arguments, counters and statistics read back, CSR offsets): DMA from / to pinned memory,
     // where pageable memory would go through a runtime staging copy -- a blit kernel that has to
     // wait for free CUs while other contexts' detection kernels hold them all
-    PinBuf h_small, h_off;
+    PinBuf h_small, h_off, h_tab, h_fo;  // (h_tab: chip tables of a launch; h_fo: row-fetch offsets)
     DevBuf<int64_t> slot_dates[CCDGPU_UPLOAD_SLOTS];   // upload slots (ccdgpu_stage_slot / ccdgpu_run_slot)
     DevBuf<int16_t> slot_spectra[CCDGPU_UPLOAD_SLOTS];
     DevBuf<uint16_t> slot_qa[CCDGPU_UPLOAD_SLOTS];
@@ -245,6 +251,9 @@ struct ccdgpu_ctx {
         h_rows.release();
         h_small.release();
         h_off.release();
+        h_tab.release();
+        h_fo.release();
+        if (aux_own && aux) (void)hipStreamDestroy(aux);
         for (auto &e : ev)
             if (e) (void)hipEventDestroy(e);
         if (done) (void)hipEventDestroy(done);
@@ -329,8 +338,11 @@ int ccdgpu_device_numa_node(int device, int *node) {
     return 0;
 }
 
-int ccdgpu_init(int device, ccdgpu_ctx **out) {
+int ccdgpu_init(int device, ccdgpu_ctx **out) { return ccdgpu_init_copy_cus(device, 0, out); }
+
+int ccdgpu_init_copy_cus(int device, int copy_cus, ccdgpu_ctx **out) {
     if (!out) return fail(CCDGPU_EINVAL, "ctx out pointer is NULL");
+    if (copy_cus < 0) return fail(CCDGPU_EINVAL, "copy_cus must be >= 0");
     *out = nullptr;
     int count = 0;
     int rc = ccdgpu_device_count(&count);
@@ -351,13 +363,13 @@ int ccdgpu_init(int device, ccdgpu_ctx **out) {
         return fail(CCDGPU_EHIP, "device " + std::to_string(device) + " is " + arch + ", libccdgpu is built for gfx950 only");
     }
     c->n_cu = prop.multiProcessorCount;
-    // CCDGPU_COPY_CUS = k > 0: the copy stream (uploads' decode kernel, blits) gets k CUs of its
-    // own -- the same k for every context -- and the detection stream the rest, so a context's
-    // upload is never starved of CUs by other contexts' persistent detection waves (which
-    // otherwise hold every wave slot until their launch drains).  Reserved: the last k / 8 CUs of
-    // each group of n_cu / 8 (one group per XCD, if the mask numbers CUs XCD-major).
-    int copy_cus = 0;
-    if (const char *e = std::getenv("CCDGPU_COPY_CUS")) copy_cus = std::atoi(e);
+    // copy_cus = k > 0: the copy stream (uploads' decode kernel, blits) gets k CUs of its own --
+    // the same k for every context -- and the detection stream the rest, so a context's upload is
+    // never starved of CUs by other contexts' persistent detection waves (which otherwise hold
+    // every wave slot until their launch drains).  Reserved: the last ceil(k / 8) CUs of each
+    // group of n_cu / 8 (one group per XCD, if the mask numbers CUs XCD-major).  The environment
+    // variable CCDGPU_COPY_CUS overrides k (experiments).
+    if (const char *e = std::getenv("CCDGPU_COPY_CUS")) copy_cus = std::max(0, std::atoi(e));
     std::vector<uint32_t> mask_det, mask_copy;
     if (copy_cus > 0 && copy_cus < c->n_cu) {
         const int nw = (c->n_cu + 31) / 32, groups = 8, per = c->n_cu / groups, k = (copy_cus + groups - 1) / groups;
@@ -382,6 +394,15 @@ int ccdgpu_init(int device, ccdgpu_ctx **out) {
         return fail(CCDGPU_EHIP, "hipStreamCreate failed");
     }
     for (auto &e : c->uploaded) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    c->aux = c->stream;
+    if (masked) {
+        if (hipExtStreamCreateWithCUMask(&c->aux, (uint32_t)mask_copy.size(), mask_copy.data()) != hipSuccess) {
+            c->aux = nullptr;
+            delete c;
+            return fail(CCDGPU_EHIP, "hipStreamCreate failed");
+        }
+        c->aux_own = true;
+    }
     c->arg_slot = acquire_arg_slot();
     if (c->arg_slot < 0) {
         delete c;
@@ -403,6 +424,7 @@ int ccdgpu_destroy(ccdgpu_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipStreamSynchronize(ctx->copy_stream);
+    if (ctx->aux) (void)hipStreamSynchronize(ctx->aux);
     delete ctx;
     return 0;
 }
@@ -467,12 +489,21 @@ static int stage_alloc(ccdgpu_ctx *c, const ccdgpu_params *params, const Shape &
         return rc;
     if (c->pool_cap < c->total_pix * 8) c->pool_cap = c->total_pix * 8;
     if ((rc = c->pool.ensure(c->pool_cap)) || (rc = c->pool_seq.ensure(c->pool_cap))) return rc;
-    // chip tables (pageable sources: the copies are staged before the calls return)
-    HIPCHK(hipMemcpyAsync(c->chip_nobs.p, sh.nobs.data(), sizeof(int32_t) * nc, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->chip_obs_off.p, sh.obs_off.data(), sizeof(int64_t) * (nc + 1), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->chip_pix_off.p, sh.pix_off.data(), sizeof(int64_t) * (nc + 1), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->chip_data_off.p, sh.data_off.data(), sizeof(int64_t) * (nc + 1), hipMemcpyHostToDevice, c->stream));
-    if (dates) HIPCHK(hipMemcpyAsync(c->dates.p, dates, sizeof(int64_t) * tobs, hipMemcpyHostToDevice, c->stream));
+    // chip tables, through the context's pinned staging (DMA, no runtime staging copy), on the
+    // aux stream that runs the launch's prep; the previous launch's table copies are done
+    HIPCHK(hipStreamSynchronize(c->aux));
+    const size_t t8 = 8 * ((size_t)nc + 1);
+    if ((rc = c->h_tab.ensure(3 * t8 + 4 * (size_t)nc))) return rc;
+    unsigned char *ht = c->h_tab.p;
+    std::memcpy(ht, sh.obs_off.data(), t8);
+    std::memcpy(ht + t8, sh.pix_off.data(), t8);
+    std::memcpy(ht + 2 * t8, sh.data_off.data(), t8);
+    std::memcpy(ht + 3 * t8, sh.nobs.data(), 4 * (size_t)nc);
+    HIPCHK(hipMemcpyAsync(c->chip_obs_off.p, ht, t8, hipMemcpyHostToDevice, c->aux));
+    HIPCHK(hipMemcpyAsync(c->chip_pix_off.p, ht + t8, t8, hipMemcpyHostToDevice, c->aux));
+    HIPCHK(hipMemcpyAsync(c->chip_data_off.p, ht + 2 * t8, t8, hipMemcpyHostToDevice, c->aux));
+    HIPCHK(hipMemcpyAsync(c->chip_nobs.p, ht + 3 * t8, 4 * (size_t)nc, hipMemcpyHostToDevice, c->aux));
+    if (dates) HIPCHK(hipMemcpyAsync(c->dates.p, dates, sizeof(int64_t) * tobs, hipMemcpyHostToDevice, c->aux));
     c->in_dates = c->dates.p;
     c->in_spectra = c->spectra.p;
     c->in_qa = c->qa.p;
@@ -660,7 +691,7 @@ int ccdgpu_run_slot(ccdgpu_ctx *c, int32_t slot, double *kernel_seconds) {
     if (slot < 0 || slot >= CCDGPU_UPLOAD_SLOTS || !c->slot_ready[slot]) return fail(CCDGPU_EINVAL, "slot has no staged batch");
     int rc = stage_alloc(c, &c->slot_params[slot], c->slot_shape[slot], nullptr, false);
     if (rc) return rc;
-    HIPCHK(hipStreamWaitEvent(c->stream, c->uploaded[slot], 0));
+    HIPCHK(hipStreamWaitEvent(c->aux, c->uploaded[slot], 0));
     c->in_dates = c->slot_dates[slot].p;
     c->in_spectra = c->slot_spectra[slot].p;
     c->in_qa = c->slot_qa[slot].p;
@@ -725,34 +756,40 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         a.pool_cap = c->pool_cap;
         // h_small: [0, 64) initial counters, [64, 128) counters back, [128, 128 + 8 NSTATS) stats
         // back, then the kernel arguments (each launch waits for the previous one's copies)
+        // [SM_ARGS + args, + 8 NSTATS) zeros for the statistics
         constexpr size_t SM_ARGS = 128 + 8 * CCD_NSTATS;
-        if (int rc0 = c->h_small.ensure(SM_ARGS + sizeof(CcdDetectArgs))) return rc0;
+        constexpr size_t SM_ZERO = SM_ARGS + ((sizeof(CcdDetectArgs) + 63) & ~(size_t)63);
+        if (int rc0 = c->h_small.ensure(SM_ZERO + 8 * CCD_NSTATS)) return rc0;
         unsigned long long *hinit = reinterpret_cast<unsigned long long *>(c->h_small.p);
         const unsigned long long init[8] = {0ull, 0ull, ~0ull, 0ull, 0ull, ~0ull, 0ull, ~0ull};
         std::memcpy(hinit, init, sizeof(init));
-        HIPCHK(hipMemcpyAsync(c->counters.p, hinit, sizeof(init), hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipMemsetAsync(c->stats.p, 0, sizeof(unsigned long long) * CCD_NSTATS, c->stream));
+        std::memset(c->h_small.p + SM_ZERO, 0, 8 * CCD_NSTATS);
+        hipStream_t ax = c->aux;
+        HIPCHK(hipMemcpyAsync(c->counters.p, hinit, sizeof(init), hipMemcpyHostToDevice, ax));
+        HIPCHK(hipMemcpyAsync(c->stats.p, c->h_small.p + SM_ZERO, 8 * CCD_NSTATS, hipMemcpyHostToDevice, ax));
         CcdDetectArgs *hargs = reinterpret_cast<CcdDetectArgs *>(c->h_small.p + SM_ARGS);
         std::memcpy(hargs, &a, sizeof(a));
-        if (ccdk_set_args(hargs, c->arg_slot, c->stream)) return fail(CCDGPU_EHIP, "copying kernel arguments to constant memory failed");
-        HIPCHK(hipEventRecord(c->ev[0], c->stream));
+        if (ccdk_set_args(hargs, c->arg_slot, ax)) return fail(CCDGPU_EHIP, "copying kernel arguments to constant memory failed");
+        HIPCHK(hipEventRecord(c->ev[0], ax));
         if (ccdk_prep(c->in_dates, nc, c->chip_nobs.p, c->chip_obs_off.p, p.avg_days_yr, c->order.p, c->sdates.p, c->basis.p,
-                      c->stream))
+                      ax))
             return fail(CCDGPU_EHIP, std::string("prep launch: ") + hipGetErrorString(hipGetLastError()));
-        HIPCHK(hipEventRecord(c->ev[1], c->stream));
+        HIPCHK(hipEventRecord(c->ev[1], ax));
+        if (ax != c->stream) HIPCHK(hipStreamWaitEvent(c->stream, c->ev[1], 0));
         if (ccdk_detect(c->n_slots, c->variant, sh.n_obs_max, c->arg_slot, c->stream))
             return fail(CCDGPU_EHIP, std::string("detect launch: ") + hipGetErrorString(hipGetLastError()));
         HIPCHK(hipEventRecord(c->ev[2], c->stream));
+        if (ax != c->stream) HIPCHK(hipStreamWaitEvent(ax, c->ev[2], 0));
         // counters and statistics back into pinned memory, then sleep until they have landed
         unsigned long long *h = reinterpret_cast<unsigned long long *>(c->h_small.p + 64);
         unsigned long long *hst = reinterpret_cast<unsigned long long *>(c->h_small.p + 128);
-        HIPCHK(hipMemcpyAsync(h, c->counters.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(hst, c->stats.p, sizeof(unsigned long long) * CCD_NSTATS, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(h, c->counters.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, ax));
+        HIPCHK(hipMemcpyAsync(hst, c->stats.p, sizeof(unsigned long long) * CCD_NSTATS, hipMemcpyDeviceToHost, ax));
         if (c->done) {
-            HIPCHK(hipEventRecord(c->done, c->stream));
+            HIPCHK(hipEventRecord(c->done, ax));
             HIPCHK(hipEventSynchronize(c->done));
         } else {
-            HIPCHK(hipStreamSynchronize(c->stream));
+            HIPCHK(hipStreamSynchronize(ax));
         }
         if (h[4] >= 100000) {
             // checking build: every call site that ran without a full EXEC, from the line bitmap
@@ -785,20 +822,20 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         int rc;
         if ((rc = c->csr.ensure(c->n_pool > 0 ? c->n_pool : 1))) return rc;
         size_t tmp_bytes = 0;
-        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, c->nseg.p, c->offsets.p, (int)c->total_pix + 1, c->stream));
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, c->nseg.p, c->offsets.p, (int)c->total_pix + 1, ax));
         if ((rc = c->cub_tmp.ensure(tmp_bytes))) return rc;
         // nseg has total_pix entries; the scan over total_pix+1 needs a trailing zero
-        HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->cub_tmp.p, tmp_bytes, c->nseg.p, c->offsets.p, (int)c->total_pix, c->stream));
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->cub_tmp.p, tmp_bytes, c->nseg.p, c->offsets.p, (int)c->total_pix, ax));
         c->h_offsets.resize(c->total_pix + 1);
         if ((rc = c->h_off.ensure(sizeof(int64_t) * (size_t)c->total_pix))) return rc;
-        HIPCHK(hipMemcpyAsync(c->h_off.p, c->offsets.p, sizeof(int64_t) * c->total_pix, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipMemcpyAsync(c->h_off.p, c->offsets.p, sizeof(int64_t) * c->total_pix, hipMemcpyDeviceToHost, ax));
+        HIPCHK(hipStreamSynchronize(ax));
         std::memcpy(c->h_offsets.data(), c->h_off.p, sizeof(int64_t) * (size_t)c->total_pix);
         c->h_offsets[c->total_pix] = c->n_pool;
-        if (ccdk_scatter(c->pool.p, c->pool_seq.p, c->n_pool, c->offsets.p, c->chip_pix_off.p, nc, c->csr.p, c->stream))
+        if (ccdk_scatter(c->pool.p, c->pool_seq.p, c->n_pool, c->offsets.p, c->chip_pix_off.p, nc, c->csr.p, ax))
             return fail(CCDGPU_EHIP, "scatter launch failed");
-        HIPCHK(hipEventRecord(c->ev[3], c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipEventRecord(c->ev[3], ax));
+        HIPCHK(hipStreamSynchronize(ax));
         c->last.detect_ms = ms_det;
         c->last.detect_ms_device = h[6] > h[5] ? (double)(h[6] - h[5]) / 1e5 : 0.0;  // 100 MHz clock
         c->last.prep_ms = ms_prep;
@@ -903,13 +940,20 @@ static int fetch_rows_range(ccdgpu_ctx *c, int32_t c0, int32_t c1, const int32_t
     if ((rc = c->rows.ensure((size_t)n_rows)) || (rc = c->row_off.ensure(np + 1)) || (rc = c->seg_off1.ensure(np + 1)) ||
         (!packed_mask && (rc = c->mask8.ensure((size_t)nd))))
         return rc;
-    HIPCHK(hipMemcpyAsync(c->seg_off1.p, soff.data(), sizeof(int64_t) * (np + 1), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->row_off.p, roff.data(), sizeof(int64_t) * (np + 1), hipMemcpyHostToDevice, c->stream));
+    // offsets through pinned staging, row packing and the copies back on the aux stream (the
+    // reserved CUs when there are: other contexts' detections hold the rest)
+    hipStream_t ax = c->aux;
+    const size_t ob = sizeof(int64_t) * (size_t)(np + 1);
+    if ((rc = c->h_fo.ensure(2 * ob))) return rc;
+    std::memcpy(c->h_fo.p, soff.data(), ob);
+    std::memcpy(c->h_fo.p + ob, roff.data(), ob);
+    HIPCHK(hipMemcpyAsync(c->seg_off1.p, c->h_fo.p, ob, hipMemcpyHostToDevice, ax));
+    HIPCHK(hipMemcpyAsync(c->row_off.p, c->h_fo.p + ob, ob, hipMemcpyHostToDevice, ax));
     for (int32_t ch = c0; ch < c1; ++ch) {
         const int64_t q = sh.pix_off[ch] - p0;
         if (ccdk_pack_rows(c->csr.p + s0, c->seg_off1.p + q, c->row_off.p + q, c->mask.p + (size_t)sh.pix_off[ch] * c->mask_words,
                            c->mask_words, sh.npix[ch], sh.nobs[ch], cx[ch - c0], cy[ch - c0], width, c->rows.p,
-                           packed_mask ? nullptr : c->mask8.p + (sh.data_off[ch] - d0), c->stream))
+                           packed_mask ? nullptr : c->mask8.p + (sh.data_off[ch] - d0), ax))
             return fail(CCDGPU_EHIP, "row packing launch failed");
     }
     out->n_pix = (int32_t)np;
@@ -936,20 +980,21 @@ static int fetch_rows_range(ccdgpu_ctx *c, int32_t c0, int32_t c1, const int32_t
         const size_t bit_bytes = sizeof(uint32_t) * nbits;
         const size_t bit_at = (row_bytes + 255) & ~(size_t)255;
         if ((rc = c->h_rows.ensure(bit_at + bit_bytes))) {
+            (void)hipStreamSynchronize(ax);
             ccdgpu_rows_free(out);
             return rc;
         }
-        HIPCHK(hipMemcpyAsync(c->h_rows.p, c->rows.p, row_bytes, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(c->h_rows.p, c->rows.p, row_bytes, hipMemcpyDeviceToHost, ax));
         HIPCHK(hipMemcpyAsync(c->h_rows.p + bit_at, c->mask.p + (size_t)p0 * c->mask_words, bit_bytes,
-                              hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
+                              hipMemcpyDeviceToHost, ax));
+        HIPCHK(hipStreamSynchronize(ax));
         std::memcpy(out->rows, c->h_rows.p, row_bytes);
         std::memcpy(out->mask_bits, c->h_rows.p + bit_at, bit_bytes);
         return 0;
     }
-    HIPCHK(hipMemcpyAsync(out->rows, c->rows.p, row_bytes, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(out->mask, c->mask8.p, (size_t)nd, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpyAsync(out->rows, c->rows.p, row_bytes, hipMemcpyDeviceToHost, ax));
+    HIPCHK(hipMemcpyAsync(out->mask, c->mask8.p, (size_t)nd, hipMemcpyDeviceToHost, ax));
+    HIPCHK(hipStreamSynchronize(ax));
     return 0;
 }
 

@@ -56,6 +56,13 @@ def test_init_without_gpu_fails_loudly():
         pytest.skip('a GPU is visible')
     with pytest.raises(ccdgpu.CcdGpuError):
         ccdgpu.Context(0)
+    with pytest.raises(ccdgpu.CcdGpuError):
+        ccdgpu.Context(0, copy_cus=8)
+
+
+def test_init_rejects_a_negative_cu_reservation():
+    with pytest.raises(ccdgpu.CcdGpuError, match='copy_cus'):
+        ccdgpu.Context(0, copy_cus=-1)
 
 
 def test_header_constants_match_the_binding():

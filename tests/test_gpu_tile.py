@@ -2,8 +2,8 @@
 ccdc/core.py:78-123): chips of the reference tile grid (test/data/tile_response.json) with
 synthetic ARD of both cadences, two contexts per GPU with pinned uploads in the transport
 encoding, device row packing, per-chip rows gathered -- checked against rows restated from the C
-oracle, and byte-identical however the chips are batched and whether they are uploaded encoded
-or raw."""
+oracle, and byte-identical however the chips are batched, whether they are uploaded encoded or
+raw and whether the contexts reserve CUs for their uploads."""
 import json
 import os
 
@@ -35,11 +35,11 @@ def source(pos):
     return ccdgpu.ChipBatch.from_chips([chip(p) for p in pos], pinned=True)
 
 
-def run(contexts, batch_chips, encode=True):
+def run(contexts, batch_chips, encode=True, copy_cus=8):
     from ccdc import runner
     sink = runner.SummarySink(keep_rows=True)
     res = runner.changedetection(tile(), source, device=0, contexts=contexts, batch_chips=batch_chips,
-                                 number=N_CHIPS, sink=sink, encode=encode)
+                                 number=N_CHIPS, sink=sink, encode=encode, copy_cus=copy_cus)
     return res, sink
 
 
@@ -66,3 +66,6 @@ def test_tile_runner_rows_match_oracle_and_batching():
     # the runner's default upload is the transport encoding: raw uploads give the same rows
     res3, _ = run(2, 4, encode=False)
     assert [c['digest'] for c in res3['chips']] == [c['digest'] for c in res['chips']]
+    # and so do contexts without CUs reserved for the upload stream (ccdgpu_init_copy_cus)
+    res4, _ = run(2, 3, copy_cus=0)
+    assert [c['digest'] for c in res4['chips']] == [c['digest'] for c in res['chips']]

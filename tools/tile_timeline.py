@@ -2,7 +2,8 @@
 """Timeline of a traced tile run (rocprofv3 --kernel-trace --memory-copy-trace, rocpd database):
 over the timed window (the last `seconds` of the trace, from bench.py's tile JSON) the fraction
 of wall time covered by at least one detection kernel, by at least one host-to-device copy, by
-both, and by neither; the H2D bytes and rate; and the detection kernels' summed durations.
+both, and by neither; the H2D bytes and rate; the detection kernels' summed durations; and the
+upload decode kernel's durations (median, max).
 
 usage: tile_timeline.py <run_results.db> <tile.json>"""
 import json
@@ -61,6 +62,7 @@ def main():
     d = clip(union(det), lo, hi)
     h = clip(union([(a, b) for a, b, _ in h2d]), lo, hi)
     nbytes = sum(n for a, b, n in h2d if a >= lo)
+    dec = [e - s for n, s, e in c.execute('select name, start, end from kernels') if 'decode_enc' in n and s >= lo]
     both = intersect(d, h)
     wall = hi - lo
     out = {'window_s': wall / 1e9, 'detect_covered': length(d) / wall, 'h2d_covered': length(h) / wall,
@@ -68,6 +70,8 @@ def main():
            'h2d_bytes': nbytes, 'h2d_gbs_over_window': nbytes / wall, 'h2d_gbs_while_copying': nbytes / max(1, length(h)),
            'detect_dispatches': sum(1 for a, b in det if a >= lo),
            'detect_kernel_seconds_summed': sum(b - a for a, b in det if a >= lo) / 1e9,
+           'decode_dispatches': len(dec), 'decode_ms_median': (sorted(dec)[len(dec) // 2] / 1e6) if dec else None,
+           'decode_ms_max': (max(dec) / 1e6) if dec else None,
            'copy_kinds': sorted({str(r[ci['name']]) for r in rows}) if 'name' in ci else cols}
     print(json.dumps(out, indent=1))
 
