@@ -109,14 +109,17 @@ __attribute__((target("avx512f,avx512bw,avx512vbmi2"))) static size_t compact_vb
 /* 4-bit palette codes (two per byte, even observation in the low nibble) and the keep bit masks
  * of one pixel's QA row, 32 observations at a time: a code is the index of the palette entry its
  * word equals (at most 16 compares); the codes' 16-bit lanes, read as 32-bit pairs, fold into
- * bytes with one down-convert. */
-__attribute__((target("avx512f,avx512bw,avx512vl,avx512vbmi2"))) static void qa_codes_avx512(const uint16_t *q, int n,
-                                                                                   const uint16_t *pal, int npal,
-                                                                                   uint16_t drop, uint16_t strict,
-                                                                                   uint8_t *r, uint32_t *km,
-                                                                                   uint32_t *sm) {
+ * bytes with one down-convert.  Returns nonzero if a word is not in the palette (it got code 0
+ * without being pal[0]): the palette came from a sample of the chip's pixels and misses it. */
+__attribute__((target("avx512f,avx512bw,avx512vl,avx512vbmi2"))) static int qa_codes_avx512(const uint16_t *q, int n,
+                                                                                  const uint16_t *pal, int npal,
+                                                                                  uint16_t drop, uint16_t strict,
+                                                                                  uint8_t *r, uint32_t *km,
+                                                                                  uint32_t *sm) {
     int i = 0, w = 0;
     const __m512i dropv = _mm512_set1_epi16((short)drop), strictv = _mm512_set1_epi16((short)strict);
+    const __m512i pal0 = _mm512_set1_epi16((short)pal[0]);
+    __mmask32 miss = 0;
     for (; i < n; i += 32, ++w) {
         const __mmask32 lm = n - i >= 32 ? (__mmask32)0xFFFFFFFFu : (__mmask32)((1u << (n - i)) - 1u);
         const __m512i v = _mm512_maskz_loadu_epi16(lm, (const void *)(q + i));
@@ -124,6 +127,7 @@ __attribute__((target("avx512f,avx512bw,avx512vl,avx512vbmi2"))) static void qa_
         for (int j = 1; j < npal; ++j)
             code = _mm512_mask_mov_epi16(code, _mm512_cmpeq_epi16_mask(v, _mm512_set1_epi16((short)pal[j])),
                                          _mm512_set1_epi16((short)j));
+        miss |= _mm512_mask_cmpneq_epi16_mask(_mm512_cmpeq_epi16_mask(code, _mm512_setzero_si512()) & lm, v, pal0);
         km[w] = (uint32_t)(_mm512_testn_epi16_mask(v, dropv) & lm);
         sm[w] = (uint32_t)(_mm512_test_epi16_mask(v, strictv) & lm);
         const __m512i pr = _mm512_or_si512(_mm512_and_si512(code, _mm512_set1_epi32(0xF)),
@@ -132,6 +136,21 @@ __attribute__((target("avx512f,avx512bw,avx512vl,avx512vbmi2"))) static void qa_
         const int nb = (n - i >= 32 ? 32 : n - i + 1) / 2;  /* bytes of this chunk's codes */
         _mm_mask_storeu_epi8(r + (i >> 1), (__mmask16)(nb == 16 ? 0xFFFFu : (1u << nb) - 1u), bytes);
     }
+    return miss != 0;
+}
+/* pass 1 of a pixel's QA row outside the palette sample: the dropped count only */
+__attribute__((target("avx512f,avx512bw,avx512vl"))) static uint32_t qa_count_avx512(const uint16_t *q, int n,
+                                                                                   uint16_t drop) {
+    uint32_t fill = 0;
+    const __m512i dv = _mm512_set1_epi16((short)drop);
+    int i = 0;
+    for (; i + 32 <= n; i += 32)
+        fill += (uint32_t)__builtin_popcount(_mm512_test_epi16_mask(_mm512_loadu_si512((const void *)(q + i)), dv));
+    if (i < n) {
+        const __mmask32 lm = (__mmask32)((1u << (n - i)) - 1u);
+        fill += (uint32_t)__builtin_popcount(_mm512_test_epi16_mask(_mm512_maskz_loadu_epi16(lm, (const void *)(q + i)), dv) & lm);
+    }
+    return fill;
 }
 /* pass 1 of one pixel's QA row, vector path: dropped count, and every word not yet in the thread's
  * list s_pal (compared 32 at a time against the list; the rare new word is added) */
@@ -218,6 +237,12 @@ static size_t encode_raw(int32_t n_pix, int32_t n_obs, const int16_t *spectra, c
     return sec_mode0(n_pix, n_obs);
 }
 
+/* pixels of a chip whose QA rows pass 1 scans for the palette (vector path): every
+ * ENC_SAMPLE-th; pass 2 checks every word against it and, when one is missing, the chip is
+ * encoded again from a scan of every pixel.  The palette is the chip's sorted set of distinct
+ * words either way, so the bytes are the same. */
+#define ENC_SAMPLE 16
+
 /* one chip into sec (room for the larger of its two modes); returns the section's bytes */
 static size_t encode_chip(int32_t n_pix, int32_t n_obs, const int16_t *spectra, const uint16_t *qa, int64_t pix_base,
                           int64_t data_off, uint8_t *sec, int threads, uint32_t *kept_scratch, uint16_t drop,
@@ -225,7 +250,7 @@ static size_t encode_chip(int32_t n_pix, int32_t n_obs, const int16_t *spectra, 
     const size_t plane = (size_t)n_pix * (size_t)n_obs;
     int nt = threads > 0 ? threads : 1;
     if (nt > 64) nt = 64;
-    pass1_t *st = (pass1_t *)calloc((size_t)nt, sizeof(pass1_t));
+    pass1_t *st = (pass1_t *)malloc((size_t)nt * sizeof(pass1_t));
     uint8_t *lut = (uint8_t *)malloc(65536);  /* QA word -> palette index */
     if (!st || !lut) {
         free(st);
@@ -233,151 +258,165 @@ static size_t encode_chip(int32_t n_pix, int32_t n_obs, const int16_t *spectra, 
         return 0;
     }
     const int vec1 = have_vbmi2();
-    /* pass 1: kept counts, distinct QA words */
+    size_t ret = 0;
+    for (int full = vec1 ? 0 : 1; full < 2; ++full) {
+        const int sample = full ? 1 : ENC_SAMPLE;
+        memset(st, 0, (size_t)nt * sizeof(pass1_t));
+        /* pass 1: kept counts, distinct QA words (of the sampled pixels) */
 #pragma omp parallel for schedule(static) num_threads(nt)
-    for (int32_t p = 0; p < n_pix; ++p) {
+        for (int32_t p = 0; p < n_pix; ++p) {
 #ifdef _OPENMP
-        pass1_t *s = &st[omp_get_thread_num()];
+            pass1_t *s = &st[omp_get_thread_num()];
 #else
-        pass1_t *s = &st[0];
+            pass1_t *s = &st[0];
 #endif
-        const uint16_t *q = qa + (size_t)p * n_obs;
-        uint32_t fill = 0;
+            const uint16_t *q = qa + (size_t)p * n_obs;
+            uint32_t fill = 0;
 #if defined(__x86_64__)
-        if (vec1) {
-            fill = qa_scan_avx512(q, n_obs, drop, s->pal, &s->npal);
-        } else
+            if (vec1) {
+                fill = p % sample == 0 ? qa_scan_avx512(q, n_obs, drop, s->pal, &s->npal) : qa_count_avx512(q, n_obs, drop);
+            } else
 #endif
-        {
-            for (int32_t i = 0; i < n_obs; ++i) {
-                const uint16_t v = q[i];
-                s->seen[v] = 1;
-                fill += (v & drop) != 0;
-            }
-        }
-        kept_scratch[p] = (uint32_t)n_obs - fill;
-    }
-    int bad = 0;  /* (pass 2 checks the fill observations' band values) */
-    uint16_t palv[16];
-    int npal = 0;
-    for (int t = 0; t < nt; ++t) bad |= st[t].bad_fill;
-    if (vec1)  /* the threads' word lists into the byte set the scalar path fills */
-        for (int t = 0; t < nt; ++t)
-            for (int j = 0; j < st[t].npal; ++j) st[t].seen[st[t].pal[j]] = 1;
-    for (int t = 0; t < nt; ++t)
-        if (st[t].npal > 16) bad = 1;  /* (vector path: one thread alone met more than 16 words) */
-    {
-        uint64_t *s0 = (uint64_t *)st[0].seen;
-        for (int t = 1; t < nt; ++t) {
-            const uint64_t *st_ = (const uint64_t *)st[t].seen;
-            for (int w = 0; w < 8192; ++w) s0[w] |= st_[w];
-        }
-        for (int w = 0; w < 8192 && npal <= 16; ++w)  /* ascending: the palette is sorted */
-            if (s0[w])
-                for (int j = 0; j < 8 && npal <= 16; ++j)
-                    if (st[0].seen[8 * w + j]) {
-                        if (npal < 16) palv[npal] = (uint16_t)(8 * w + j);
-                        ++npal;
-                    }
-    }
-    free(st);
-    int32_t *h = (int32_t *)sec;
-    memset(sec, 0, ENC_HDR);
-    h[1] = n_pix;
-    h[2] = n_obs;
-    int64_t *h64 = (int64_t *)(sec + 48);
-    h64[1] = data_off;
-    h64[3] = pix_base;
-    if (bad || npal > 16) {
-        free(lut);
-        return encode_raw(n_pix, n_obs, spectra, qa, sec, nt);
-    }
-    h[0] = 1;
-    h[3] = npal;
-    *(uint32_t *)(sec + 80) = drop;  /* the decoder's keep test */
-    uint16_t *pal = (uint16_t *)(sec + 16);
-    for (int j = 0; j < npal; ++j) {
-        pal[j] = palv[j];
-        lut[palv[j]] = (uint8_t)j;
-    }
-    uint32_t *koff = (uint32_t *)(sec + ENC_HDR);
-    uint64_t tot = 0;
-    for (int32_t p = 0; p < n_pix; ++p) {
-        koff[p] = (uint32_t)tot;
-        tot += kept_scratch[p];
-    }
-    koff[n_pix] = (uint32_t)tot;
-    const size_t bstride = up((size_t)tot, 8);
-    h64[0] = (int64_t)tot;
-    h64[2] = (int64_t)bstride;
-    uint8_t *q4 = sec + ENC_HDR + up(4 * ((size_t)n_pix + 1), 16);
-    const size_t rowb = (size_t)(n_obs + 1) / 2;
-    int16_t *bands = (int16_t *)(q4 + up((size_t)n_pix * rowb, 16));
-    const int vec = have_vbmi2();
-    int bad2 = 0;
-    /* pass 2: 4-bit QA codes and the kept band values (and the fill observations' values checked).
-     * Vector path in blocks of enc_block() pixels: the block's keep / strict masks first, then one
-     * band at a time over the whole block, so the loads and stores run as two long sequential
-     * streams (band rows of consecutive pixels are contiguous in the input plane and in the
-     * output) instead of seven of each interleaved per pixel. */
-    const int mw = n_obs / 32 + 2;  /* mask words per pixel */
-    const int pb = enc_block();
-#pragma omp parallel num_threads(nt) reduction(| : bad2)
-    {
-        uint8_t *keep = (uint8_t *)malloc(2 * (size_t)n_obs + 64), *strictm = keep + n_obs + 32;
-        uint32_t *km = (uint32_t *)malloc((size_t)mw * 8 * pb), *sm = km + (size_t)mw * pb;
-#if defined(__x86_64__)
-        if (vec) {
-#pragma omp for schedule(static)
-            for (int32_t p0 = 0; p0 < n_pix; p0 += pb) {
-                const int32_t pe = p0 + pb < n_pix ? p0 + pb : n_pix;
-                for (int32_t p = p0; p < pe; ++p)
-                    qa_codes_avx512(qa + (size_t)p * n_obs, n_obs, pal, npal, drop, strict, q4 + (size_t)p * rowb,
-                                    km + (size_t)(p - p0) * mw, sm + (size_t)(p - p0) * mw);
-                for (int b = 0; b < 7; ++b) {
-                    const int16_t *src = spectra + (size_t)b * plane;
-                    int16_t *dst = bands + (size_t)b * bstride;
-                    for (int32_t p = p0; p < pe; ++p)
-                        compact_vbmi2(src + (size_t)p * n_obs, km + (size_t)(p - p0) * mw, sm + (size_t)(p - p0) * mw,
-                                      n_obs, dst + koff[p], &bad2);
+            {
+                for (int32_t i = 0; i < n_obs; ++i) {
+                    const uint16_t v = q[i];
+                    s->seen[v] = 1;
+                    fill += (v & drop) != 0;
                 }
             }
-        } else
+            kept_scratch[p] = (uint32_t)n_obs - fill;
+        }
+        int bad = 0;  /* (pass 2 checks the fill observations' band values) */
+        uint16_t palv[16];
+        int npal = 0;
+        for (int t = 0; t < nt; ++t) bad |= st[t].bad_fill;
+        if (vec1)  /* the threads' word lists into the byte set the scalar path fills */
+            for (int t = 0; t < nt; ++t)
+                for (int j = 0; j < st[t].npal; ++j) st[t].seen[st[t].pal[j]] = 1;
+        for (int t = 0; t < nt; ++t)
+            if (st[t].npal > 16) bad = 1;  /* (vector path: one thread alone met more than 16 words) */
+        {
+            uint64_t *s0 = (uint64_t *)st[0].seen;
+            for (int t = 1; t < nt; ++t) {
+                const uint64_t *st_ = (const uint64_t *)st[t].seen;
+                for (int w = 0; w < 8192; ++w) s0[w] |= st_[w];
+            }
+            for (int w = 0; w < 8192 && npal <= 16; ++w)  /* ascending: the palette is sorted */
+                if (s0[w])
+                    for (int j = 0; j < 8 && npal <= 16; ++j)
+                        if (st[0].seen[8 * w + j]) {
+                            if (npal < 16) palv[npal] = (uint16_t)(8 * w + j);
+                            ++npal;
+                        }
+        }
+        int32_t *h = (int32_t *)sec;
+        memset(sec, 0, ENC_HDR);
+        h[1] = n_pix;
+        h[2] = n_obs;
+        int64_t *h64 = (int64_t *)(sec + 48);
+        h64[1] = data_off;
+        h64[3] = pix_base;
+        if (bad || npal > 16) {
+            ret = encode_raw(n_pix, n_obs, spectra, qa, sec, nt);
+            break;
+        }
+        h[0] = 1;
+        h[3] = npal;
+        *(uint32_t *)(sec + 80) = drop;  /* the decoder's keep test */
+        uint16_t *pal = (uint16_t *)(sec + 16);
+        for (int j = 0; j < npal; ++j) {
+            pal[j] = palv[j];
+            lut[palv[j]] = (uint8_t)j;
+        }
+        uint32_t *koff = (uint32_t *)(sec + ENC_HDR);
+        uint64_t tot = 0;
+        for (int32_t p = 0; p < n_pix; ++p) {
+            koff[p] = (uint32_t)tot;
+            tot += kept_scratch[p];
+        }
+        koff[n_pix] = (uint32_t)tot;
+        const size_t bstride = up((size_t)tot, 8);
+        h64[0] = (int64_t)tot;
+        h64[2] = (int64_t)bstride;
+        uint8_t *q4 = sec + ENC_HDR + up(4 * ((size_t)n_pix + 1), 16);
+        const size_t rowb = (size_t)(n_obs + 1) / 2;
+        int16_t *bands = (int16_t *)(q4 + up((size_t)n_pix * rowb, 16));
+        const int vec = have_vbmi2();
+        int bad2 = 0, miss = 0;
+        /* pass 2: 4-bit QA codes and the kept band values (and the fill observations' values checked).
+         * Vector path in blocks of enc_block() pixels: the block's keep / strict masks first, then one
+         * band at a time over the whole block, so the loads and stores run as two long sequential
+         * streams (band rows of consecutive pixels are contiguous in the input plane and in the
+         * output) instead of seven of each interleaved per pixel. */
+        const int mw = n_obs / 32 + 2;  /* mask words per pixel */
+        const int pb = enc_block();
+#pragma omp parallel num_threads(nt) reduction(| : bad2, miss)
+        {
+            uint8_t *keep = (uint8_t *)malloc(2 * (size_t)n_obs + 64), *strictm = keep + n_obs + 32;
+            uint32_t *km = (uint32_t *)malloc((size_t)mw * 8 * pb), *sm = km + (size_t)mw * pb;
+#if defined(__x86_64__)
+            if (vec) {
+#pragma omp for schedule(static)
+                for (int32_t p0 = 0; p0 < n_pix; p0 += pb) {
+                    const int32_t pe = p0 + pb < n_pix ? p0 + pb : n_pix;
+                    for (int32_t p = p0; p < pe; ++p)
+                        miss |= qa_codes_avx512(qa + (size_t)p * n_obs, n_obs, pal, npal, drop, strict, q4 + (size_t)p * rowb,
+                                                km + (size_t)(p - p0) * mw, sm + (size_t)(p - p0) * mw);
+                    if (miss) continue;  /* the chip is encoded again */
+                    for (int b = 0; b < 7; ++b) {
+                        const int16_t *src = spectra + (size_t)b * plane;
+                        int16_t *dst = bands + (size_t)b * bstride;
+                        for (int32_t p = p0; p < pe; ++p)
+                            compact_vbmi2(src + (size_t)p * n_obs, km + (size_t)(p - p0) * mw, sm + (size_t)(p - p0) * mw,
+                                          n_obs, dst + koff[p], &bad2);
+                    }
+                }
+            } else
 #endif
 #pragma omp for schedule(static)
-        for (int32_t p = 0; p < n_pix; ++p) {
-            const uint16_t *q = qa + (size_t)p * n_obs;
-            uint8_t *r = q4 + (size_t)p * rowb;
-            memset(km, 0, ((size_t)n_obs / 32 + 1) * 4);
-            int32_t i = 0;
-            for (; i + 1 < n_obs; i += 2) {
-                const uint16_t v0 = q[i], v1 = q[i + 1];
-                r[i >> 1] = (uint8_t)(lut[v0] | (lut[v1] << 4));
-                const uint32_t k0 = !(v0 & drop), k1 = !(v1 & drop);
-                keep[i] = (uint8_t)k0;
-                keep[i + 1] = (uint8_t)k1;
-                strictm[i] = (uint8_t)((v0 & strict) != 0);
-                strictm[i + 1] = (uint8_t)((v1 & strict) != 0);
-                km[i >> 5] |= (k0 | (k1 << 1)) << (i & 31);
+            for (int32_t p = 0; p < n_pix; ++p) {
+                const uint16_t *q = qa + (size_t)p * n_obs;
+                uint8_t *r = q4 + (size_t)p * rowb;
+                memset(km, 0, ((size_t)n_obs / 32 + 1) * 4);
+                int32_t i = 0;
+                for (; i + 1 < n_obs; i += 2) {
+                    const uint16_t v0 = q[i], v1 = q[i + 1];
+                    r[i >> 1] = (uint8_t)(lut[v0] | (lut[v1] << 4));
+                    const uint32_t k0 = !(v0 & drop), k1 = !(v1 & drop);
+                    keep[i] = (uint8_t)k0;
+                    keep[i + 1] = (uint8_t)k1;
+                    strictm[i] = (uint8_t)((v0 & strict) != 0);
+                    strictm[i + 1] = (uint8_t)((v1 & strict) != 0);
+                    km[i >> 5] |= (k0 | (k1 << 1)) << (i & 31);
+                }
+                if (i < n_obs) {
+                    const uint16_t v0 = q[i];
+                    r[i >> 1] = lut[v0];
+                    const uint32_t k0 = !(v0 & drop);
+                    keep[i] = (uint8_t)k0;
+                    strictm[i] = (uint8_t)((v0 & strict) != 0);
+                    km[i >> 5] |= k0 << (i & 31);
+                }
+                for (int b = 0; b < 7; ++b)
+                    compact_scalar(spectra + (size_t)b * plane + (size_t)p * n_obs, keep, strictm, n_obs,
+                                   bands + (size_t)b * bstride + koff[p], &bad2);
             }
-            if (i < n_obs) {
-                const uint16_t v0 = q[i];
-                r[i >> 1] = lut[v0];
-                const uint32_t k0 = !(v0 & drop);
-                keep[i] = (uint8_t)k0;
-                strictm[i] = (uint8_t)((v0 & strict) != 0);
-                km[i >> 5] |= k0 << (i & 31);
-            }
-            for (int b = 0; b < 7; ++b)
-                compact_scalar(spectra + (size_t)b * plane + (size_t)p * n_obs, keep, strictm, n_obs,
-                               bands + (size_t)b * bstride + koff[p], &bad2);
+            free(keep);
+            free(km);
         }
-        free(keep);
-        free(km);
+        if (miss && !full) continue;  /* a word the sample missed: every pixel's words this time */
+        if (bad2) {
+            ret = encode_raw(n_pix, n_obs, spectra, qa, sec, nt);  /* a strict observation with data */
+            break;
+        }
+        for (int b = 0; b < 7; ++b)  /* band padding (the scalar path may have written a dropped value there) */
+            memset(bands + (size_t)b * bstride + tot, 0, 2 * (bstride - (size_t)tot));
+        ret = sec_mode1(n_pix, n_obs, (int64_t)tot);
+        break;
     }
+    free(st);
     free(lut);
-    if (bad2) return encode_raw(n_pix, n_obs, spectra, qa, sec, nt);  /* a strict observation with data */
-    return sec_mode1(n_pix, n_obs, (int64_t)tot);
+    return ret;
 }
 
 int64_t ccdgpu_encode_chips(int32_t n_chips, const int32_t *n_pix, const int32_t *n_obs, const int16_t *const *spectra,

@@ -113,3 +113,35 @@ def test_encode_rejects_a_short_buffer():
     e.buf = e.buf[:100]
     with pytest.raises(ValueError):
         e.fill([(d, s, q)])
+
+
+def test_word_outside_the_palette_sample_reencodes_the_same_bytes():
+    """The vector encoder takes the palette from every 16th pixel's QA row and re-encodes a chip
+    whose other rows hold a word the sample missed: the result decodes to the inputs and matches
+    the scalar encoder (which scans every row) byte for byte."""
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); import ccdgpu; "
+            "n = 45; rng = np.random.default_rng(3); d = np.arange(n, dtype=np.int64) * 16 + 730000; "
+            "q = np.full((40, n), 322, dtype=np.uint16); q[5, 3] = 324; q[17, 0] = 480; q[39, n - 1] = 1; "
+            "s = rng.integers(0, 5000, size=(7, 40, n)).astype(np.int16); s[:, 39, n - 1] = -9999; "
+            "e = ccdgpu.EncodedBatch.encode([(d, s, q)], threads=2, pinned=False); "
+            "sys.stdout.buffer.write(bytes([int(ccdgpu.encode_vector_path())]) + e.buf[:e.nbytes_encoded].tobytes())"
+            % os.path.join(ROOT, 'lcmap-firebird_amd'))
+    outs = {}
+    for scalar in ('0', '1'):
+        env = dict(os.environ, CCDGPU_ENCODE_SCALAR=scalar)
+        outs[scalar] = subprocess.run([sys.executable, '-c', code], env=env, capture_output=True, check=True).stdout
+    buf = np.frombuffer(outs['0'][1:], dtype=np.uint8)
+    rng = np.random.default_rng(3)
+    n = 45
+    q = np.full((40, n), 322, dtype=np.uint16)
+    q[5, 3] = 324
+    q[17, 0] = 480
+    q[39, n - 1] = 1
+    s = rng.integers(0, 5000, size=(7, 40, n)).astype(np.int16)
+    s[:, 39, n - 1] = -9999
+    (ds, dq), = decode(buf)
+    np.testing.assert_array_equal(ds, s)
+    np.testing.assert_array_equal(dq, q)
+    if outs['0'][0] == 0:
+        pytest.skip('no AVX-512 VBMI2 on this CPU: only the scalar encoder ran')
+    assert outs['0'][1:] == outs['1'][1:]
