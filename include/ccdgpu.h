@@ -218,6 +218,15 @@ int ccdgpu_stage_slot_chips(ccdgpu_ctx *ctx, int32_t slot, const ccdgpu_params *
 int ccdgpu_stage_slot(ccdgpu_ctx *ctx, int32_t slot, const ccdgpu_params *params, int32_t n_chips, int32_t n_pix,
                       int32_t n_obs, const int64_t *dates, const int16_t *spectra, const uint16_t *qa);
 int ccdgpu_run_slot(ccdgpu_ctx *ctx, int32_t slot, double *kernel_seconds);
+/* ccdgpu_run_slot in two halves, so the calling thread can stage further slots while the
+ * detection runs: _begin launches it and returns at once, ccdgpu_run_query returns 1 once it has
+ * completed (0 while it runs; 1 with nothing begun), _end waits for it and does the rest of
+ * ccdgpu_run_slot (status, CSR of the segments; same return codes).  Between _begin and _end only
+ * ccdgpu_stage_slot* of other slots and ccdgpu_run_query may be called on the context.  The tile
+ * driver (ccdc.runner) stages the batches its fetch thread finishes during the detection. */
+int ccdgpu_run_slot_begin(ccdgpu_ctx *ctx, int32_t slot);
+int ccdgpu_run_query(ccdgpu_ctx *ctx);
+int ccdgpu_run_slot_end(ccdgpu_ctx *ctx, double *kernel_seconds);
 
 /* Transport-encoded uploads (no reference counterpart -- the tile path's PCIe link is its bound,
  * DESIGN.md §5).  ccdgpu_encode_chips packs chips given as per-chip pointers (spectra

@@ -332,6 +332,7 @@ def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, er
         clock = time.perf_counter
         free = list(range(depth + 1))
         staged = []  # (slot, positions, batch), in upload order
+        split = hasattr(ctx, 'run_slot_begin')  # (test doubles have run_slot only)
         exhausted = False
         while True:
             while free and not exhausted:
@@ -356,7 +357,30 @@ def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, er
                 break
             s, ppos, pbatch = staged.pop(0)
             t2 = clock()
-            ctx.run_slot(s)
+            t_in = 0.0  # staging done while the detection ran
+            if split:
+                ctx.run_slot_begin(s)
+                # while it runs, upload what the fetch thread finishes into the free slots (a
+                # batch otherwise waits for this detection and its row fetch to end)
+                while free and not exhausted and not ctx.run_done():
+                    try:
+                        item = ready.get(timeout=0.002)
+                    except queue_mod.Empty:
+                        continue
+                    if item is None:
+                        exhausted = True
+                        break
+                    if isinstance(item, BaseException):
+                        raise item
+                    pos, batch = item
+                    t1 = clock()
+                    slot = free.pop(0)
+                    ctx.stage_slot_chips(slot, batch, params)
+                    staged.append((slot, pos, batch))
+                    t_in += clock() - t1
+                ctx.run_slot_end()
+            else:
+                ctx.run_slot(s)
             if getattr(ctx, 'qa_error', False):
                 import ccdgpu
                 raise ccdgpu.QAValueError('unsupported bit-packed QA value in chips at tile positions %s' % (ppos,))
@@ -381,7 +405,8 @@ def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, er
                 stats['chips'] += len(ppos)
                 stats['pixels'] += pbatch.total_pixels
                 stats['rows'] += int(rows.shape[0])
-                stats['device_seconds'] += t3 - t2
+                stats['device_seconds'] += t3 - t2 - t_in
+                stats['stage_seconds'] += t_in
                 stats['fetch_seconds'] += t4 - t3
                 stats['sink_seconds'] += t5 - t4
     except BaseException as e:  # reported by detect_tile after the other workers drain

@@ -38,6 +38,13 @@ def _declare(L):
     L.ccdgpu_last_error.restype = c.c_char_p
     L.ccdgpu_params_default.argtypes = [c.POINTER(abi.Params)]
     L.ccdgpu_init.argtypes = [c.c_int, c.POINTER(c.c_void_p)]
+    if hasattr(L, 'ccdgpu_run_slot_begin'):
+        L.ccdgpu_run_slot_begin.argtypes = [c.c_void_p, c.c_int32]
+        L.ccdgpu_run_slot_begin.restype = c.c_int
+        L.ccdgpu_run_query.argtypes = [c.c_void_p]
+        L.ccdgpu_run_query.restype = c.c_int
+        L.ccdgpu_run_slot_end.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
+        L.ccdgpu_run_slot_end.restype = c.c_int
     if hasattr(L, 'ccdgpu_init_copy_cus'):
         L.ccdgpu_init_copy_cus.argtypes = [c.c_int, c.c_int, c.POINTER(c.c_void_p)]
         L.ccdgpu_init_copy_cus.restype = c.c_int
@@ -99,7 +106,8 @@ EXPORTS = ('ccdgpu_version', 'ccdgpu_last_error', 'ccdgpu_params_default', 'ccdg
            'ccdgpu_host_alloc', 'ccdgpu_host_free', 'ccdgpu_stage_slot', 'ccdgpu_run_slot',
            'ccdgpu_last_stats', 'ccdgpu_diag_counters', 'ccdgpu_stage_chips', 'ccdgpu_stage_slot_chips',
            'ccdgpu_fetch_batch_rows', 'ccdgpu_device_numa_node', 'ccdgpu_encoded_bound', 'ccdgpu_encode_chips',
-           'ccdgpu_encode_vector_path', 'ccdgpu_stage_slot_encoded', 'ccdgpu_init_copy_cus')
+           'ccdgpu_encode_vector_path', 'ccdgpu_stage_slot_encoded', 'ccdgpu_init_copy_cus',
+           'ccdgpu_run_slot_begin', 'ccdgpu_run_query', 'ccdgpu_run_slot_end')
 
 
 def lib():
@@ -498,6 +506,31 @@ class Context(object):
             _check(rc)
         self.qa_error = rc == abi.E_QA  # results exist; the pixel's procedure is -1 (fetch)
         self._keep = self._slot_keep.get(int(slot))
+        self._n_pix = None if isinstance(self._keep, ChipBatch) else self._keep[2].shape[1]
+        return secs.value
+
+    def run_slot_begin(self, slot):
+        """run_slot in halves (ccdgpu_run_slot_begin / _query / _end): launch the detection of
+        slot ``slot`` and return at once; run_done() says whether it has completed, and
+        run_slot_end() waits for it and finishes as run_slot does.  In between, only stage_slot*
+        of other slots may be called."""
+        _check(lib().ccdgpu_run_slot_begin(self._ctx, int(slot)))
+        self._pending_slot = int(slot)
+
+    def run_done(self):
+        rc = lib().ccdgpu_run_query(self._ctx)
+        if rc < 0:
+            _check(rc)
+        return rc == 1
+
+    def run_slot_end(self):
+        secs = ctypes.c_double(0.0)
+        rc = lib().ccdgpu_run_slot_end(self._ctx, ctypes.byref(secs))
+        if rc not in (0, abi.E_QA):
+            _check(rc)
+        self.qa_error = rc == abi.E_QA
+        slot = self._pending_slot
+        self._keep = self._slot_keep.get(slot)
         self._n_pix = None if isinstance(self._keep, ChipBatch) else self._keep[2].shape[1]
         return secs.value
 

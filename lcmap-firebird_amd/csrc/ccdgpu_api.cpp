@@ -222,6 +222,9 @@ struct ccdgpu_ctx {
     std::vector<int64_t> h_offsets;
     ccdgpu_stats last{};
     unsigned long long diag[CCD_NSTATS] = {};
+    // a detection launched by ccdgpu_run_slot_begin and not yet finished by ccdgpu_run_slot_end
+    bool pending = false;
+    CcdDetectArgs pend_args{};
     ~ccdgpu_ctx() {
         for (auto *b : {&dates, &sdates, &offsets, &chip_obs_off, &chip_pix_off, &chip_data_off, &row_off, &seg_off1, &b64_off})
             b->release();
@@ -686,8 +689,9 @@ int ccdgpu_stage_slot(ccdgpu_ctx *c, int32_t slot, const ccdgpu_params *params, 
     return ccdgpu_stage_slot_chips(c, slot, params, n_chips, np.data(), no.data(), dates, spectra, qa);
 }
 
-int ccdgpu_run_slot(ccdgpu_ctx *c, int32_t slot, double *kernel_seconds) {
+static int slot_inputs(ccdgpu_ctx *c, int32_t slot) {
     if (!c) return fail(CCDGPU_EINVAL, "NULL ctx");
+    if (c->pending) return fail(CCDGPU_EINVAL, "a detection begun with ccdgpu_run_slot_begin is not finished");
     if (slot < 0 || slot >= CCDGPU_UPLOAD_SLOTS || !c->slot_ready[slot]) return fail(CCDGPU_EINVAL, "slot has no staged batch");
     int rc = stage_alloc(c, &c->slot_params[slot], c->slot_shape[slot], nullptr, false);
     if (rc) return rc;
@@ -698,7 +702,49 @@ int ccdgpu_run_slot(ccdgpu_ctx *c, int32_t slot, double *kernel_seconds) {
     c->staged = true;
     c->ran = false;
     c->slot_ready[slot] = false;
-    return ccdgpu_run_staged(c, kernel_seconds);
+    return 0;
+}
+
+int ccdgpu_run_slot(ccdgpu_ctx *c, int32_t slot, double *kernel_seconds) {
+    int rc = slot_inputs(c, slot);
+    return rc ? rc : ccdgpu_run_staged(c, kernel_seconds);
+}
+
+static void detect_args(ccdgpu_ctx *c, CcdDetectArgs &a);
+static int launch(ccdgpu_ctx *c, CcdDetectArgs &a);
+static int finish(ccdgpu_ctx *c, double *kernel_seconds, bool *again);
+
+int ccdgpu_run_slot_begin(ccdgpu_ctx *c, int32_t slot) {
+    int rc = slot_inputs(c, slot);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(c->device));
+    detect_args(c, c->pend_args);
+    if ((rc = launch(c, c->pend_args))) return rc;
+    c->pending = true;
+    return 0;
+}
+
+int ccdgpu_run_query(ccdgpu_ctx *c) {
+    if (!c) return fail(CCDGPU_EINVAL, "NULL ctx");
+    if (!c->pending) return 1;
+    const hipError_t e = hipEventQuery(c->done);
+    if (e == hipSuccess) return 1;
+    if (e == hipErrorNotReady) return 0;
+    return fail(CCDGPU_EHIP, std::string("hipEventQuery: ") + hipGetErrorString(e));
+}
+
+int ccdgpu_run_slot_end(ccdgpu_ctx *c, double *kernel_seconds) {
+    if (!c) return fail(CCDGPU_EINVAL, "NULL ctx");
+    if (!c->pending) return fail(CCDGPU_EINVAL, "no detection begun with ccdgpu_run_slot_begin");
+    HIPCHK(hipSetDevice(c->device));
+    c->pending = false;
+    for (int attempt = 0; attempt < 4; ++attempt) {
+        bool again = false;
+        const int rc = finish(c, kernel_seconds, &again);
+        if (!again) return rc;
+        if (int rc2 = launch(c, c->pend_args)) return rc2;
+    }
+    return fail(CCDGPU_EOVERFLOW, "segment pool kept overflowing");
 }
 
 int ccdgpu_staged_inputs(ccdgpu_ctx *c, int16_t *spectra, uint16_t *qa) {
@@ -712,13 +758,10 @@ int ccdgpu_staged_inputs(ccdgpu_ctx *c, int16_t *spectra, uint16_t *qa) {
     return 0;
 }
 
-int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
-    if (!c || !c->staged) return fail(CCDGPU_EINVAL, "nothing staged");
-    HIPCHK(hipSetDevice(c->device));
+static void detect_args(ccdgpu_ctx *c, CcdDetectArgs &a) {
     const ccdgpu_params &p = c->params;
     const Shape &sh = c->shape;
     const int nc = sh.n_chips();
-    CcdDetectArgs a;
     std::memset(&a, 0, sizeof(a));
     a.p = p;
     a.n_chips = nc;
@@ -750,114 +793,145 @@ int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
         if (k <= p.peek_size) a.thr_table[k] = p.change_threshold;
         else a.thr_table[k] = chi2_5_ppf(1.0 - std::pow(1.0 - p.change_probability, (double)p.peek_size / k));
     }
-    for (int attempt = 0; attempt < 4; ++attempt) {
-        a.pool = c->pool.p;
-        a.pool_seq = c->pool_seq.p;
-        a.pool_cap = c->pool_cap;
-        // h_small: [0, 64) initial counters, [64, 128) counters back, [128, 128 + 8 NSTATS) stats
-        // back, then the kernel arguments (each launch waits for the previous one's copies)
-        // [SM_ARGS + args, + 8 NSTATS) zeros for the statistics
-        constexpr size_t SM_ARGS = 128 + 8 * CCD_NSTATS;
-        constexpr size_t SM_ZERO = SM_ARGS + ((sizeof(CcdDetectArgs) + 63) & ~(size_t)63);
-        if (int rc0 = c->h_small.ensure(SM_ZERO + 8 * CCD_NSTATS)) return rc0;
-        unsigned long long *hinit = reinterpret_cast<unsigned long long *>(c->h_small.p);
-        const unsigned long long init[8] = {0ull, 0ull, ~0ull, 0ull, 0ull, ~0ull, 0ull, ~0ull};
-        std::memcpy(hinit, init, sizeof(init));
-        std::memset(c->h_small.p + SM_ZERO, 0, 8 * CCD_NSTATS);
-        hipStream_t ax = c->aux;
-        HIPCHK(hipMemcpyAsync(c->counters.p, hinit, sizeof(init), hipMemcpyHostToDevice, ax));
-        HIPCHK(hipMemcpyAsync(c->stats.p, c->h_small.p + SM_ZERO, 8 * CCD_NSTATS, hipMemcpyHostToDevice, ax));
-        CcdDetectArgs *hargs = reinterpret_cast<CcdDetectArgs *>(c->h_small.p + SM_ARGS);
-        std::memcpy(hargs, &a, sizeof(a));
-        if (ccdk_set_args(hargs, c->arg_slot, ax)) return fail(CCDGPU_EHIP, "copying kernel arguments to constant memory failed");
-        HIPCHK(hipEventRecord(c->ev[0], ax));
-        if (ccdk_prep(c->in_dates, nc, c->chip_nobs.p, c->chip_obs_off.p, p.avg_days_yr, c->order.p, c->sdates.p, c->basis.p,
-                      ax))
-            return fail(CCDGPU_EHIP, std::string("prep launch: ") + hipGetErrorString(hipGetLastError()));
-        HIPCHK(hipEventRecord(c->ev[1], ax));
-        if (ax != c->stream) HIPCHK(hipStreamWaitEvent(c->stream, c->ev[1], 0));
-        if (ccdk_detect(c->n_slots, c->variant, sh.n_obs_max, c->arg_slot, c->stream))
-            return fail(CCDGPU_EHIP, std::string("detect launch: ") + hipGetErrorString(hipGetLastError()));
-        HIPCHK(hipEventRecord(c->ev[2], c->stream));
-        if (ax != c->stream) HIPCHK(hipStreamWaitEvent(ax, c->ev[2], 0));
-        // counters and statistics back into pinned memory, then sleep until they have landed
-        unsigned long long *h = reinterpret_cast<unsigned long long *>(c->h_small.p + 64);
-        unsigned long long *hst = reinterpret_cast<unsigned long long *>(c->h_small.p + 128);
-        HIPCHK(hipMemcpyAsync(h, c->counters.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, ax));
-        HIPCHK(hipMemcpyAsync(hst, c->stats.p, sizeof(unsigned long long) * CCD_NSTATS, hipMemcpyDeviceToHost, ax));
-        if (c->done) {
-            HIPCHK(hipEventRecord(c->done, ax));
-            HIPCHK(hipEventSynchronize(c->done));
-        } else {
-            HIPCHK(hipStreamSynchronize(ax));
-        }
-        if (h[4] >= 100000) {
-            // checking build: every call site that ran without a full EXEC, from the line bitmap
-            // (bit = line / 2) in stats[8 ..]
-            const unsigned long long *st = hst;
-            std::string lines;
-            for (int w = 8; w < CCD_NSTATS; ++w)
-                for (int b = 0; b < 64; ++b)
-                    if ((st[w] >> b) & 1ull) {
-                        const int l0 = 2 * (64 * (w - 8) + b);
-                        lines += (lines.empty() ? "" : ", ") + std::to_string(l0) + "-" + std::to_string(l0 + 1);
-                    }
-            return fail(CCDGPU_EHIP, "cross-lane primitive ran without a full EXEC at ccd_kernels.hip line " +
-                                         std::to_string(h[4] - 100000) + " (all call sites: lines " + lines + ")");
-        }
-        if (h[4]) return fail(CCDGPU_EHIP, "kernel index guard tripped at ccd_kernels.hip line " + std::to_string(h[4]));
-        if (h[3]) {  // pool overflow: grow and rerun
-            c->pool_cap = (int64_t)(h[1] + h[1] / 4 + 1024);
-            int rc;
-            if ((rc = c->pool.ensure(c->pool_cap)) || (rc = c->pool_seq.ensure(c->pool_cap))) return rc;
-            continue;
-        }
-        c->n_pool = (int64_t)h[1];
-        float ms_prep = 0.f, ms_det = 0.f;
-        (void)hipEventElapsedTime(&ms_prep, c->ev[0], c->ev[1]);
-        (void)hipEventElapsedTime(&ms_det, c->ev[1], c->ev[2]);
+}
+
+static int launch(ccdgpu_ctx *c, CcdDetectArgs &a) {
+    const ccdgpu_params &p = c->params;
+    const Shape &sh = c->shape;
+    const int nc = sh.n_chips();
+    a.pool = c->pool.p;
+    a.pool_seq = c->pool_seq.p;
+    a.pool_cap = c->pool_cap;
+    // h_small: [0, 64) initial counters, [64, 128) counters back, [128, 128 + 8 NSTATS) stats
+    // back, then the kernel arguments (each launch waits for the previous one's copies)
+    // [SM_ARGS + args, + 8 NSTATS) zeros for the statistics
+    constexpr size_t SM_ARGS = 128 + 8 * CCD_NSTATS;
+    constexpr size_t SM_ZERO = SM_ARGS + ((sizeof(CcdDetectArgs) + 63) & ~(size_t)63);
+    if (int rc0 = c->h_small.ensure(SM_ZERO + 8 * CCD_NSTATS)) return rc0;
+    unsigned long long *hinit = reinterpret_cast<unsigned long long *>(c->h_small.p);
+    const unsigned long long init[8] = {0ull, 0ull, ~0ull, 0ull, 0ull, ~0ull, 0ull, ~0ull};
+    std::memcpy(hinit, init, sizeof(init));
+    std::memset(c->h_small.p + SM_ZERO, 0, 8 * CCD_NSTATS);
+    hipStream_t ax = c->aux;
+    HIPCHK(hipMemcpyAsync(c->counters.p, hinit, sizeof(init), hipMemcpyHostToDevice, ax));
+    HIPCHK(hipMemcpyAsync(c->stats.p, c->h_small.p + SM_ZERO, 8 * CCD_NSTATS, hipMemcpyHostToDevice, ax));
+    CcdDetectArgs *hargs = reinterpret_cast<CcdDetectArgs *>(c->h_small.p + SM_ARGS);
+    std::memcpy(hargs, &a, sizeof(a));
+    if (ccdk_set_args(hargs, c->arg_slot, ax)) return fail(CCDGPU_EHIP, "copying kernel arguments to constant memory failed");
+    HIPCHK(hipEventRecord(c->ev[0], ax));
+    if (ccdk_prep(c->in_dates, nc, c->chip_nobs.p, c->chip_obs_off.p, p.avg_days_yr, c->order.p, c->sdates.p, c->basis.p,
+                  ax))
+        return fail(CCDGPU_EHIP, std::string("prep launch: ") + hipGetErrorString(hipGetLastError()));
+    HIPCHK(hipEventRecord(c->ev[1], ax));
+    if (ax != c->stream) HIPCHK(hipStreamWaitEvent(c->stream, c->ev[1], 0));
+    if (ccdk_detect(c->n_slots, c->variant, sh.n_obs_max, c->arg_slot, c->stream))
+        return fail(CCDGPU_EHIP, std::string("detect launch: ") + hipGetErrorString(hipGetLastError()));
+    HIPCHK(hipEventRecord(c->ev[2], c->stream));
+    if (ax != c->stream) HIPCHK(hipStreamWaitEvent(ax, c->ev[2], 0));
+    // counters and statistics back into pinned memory; `done` marks their arrival (finish sleeps on it)
+    unsigned long long *h = reinterpret_cast<unsigned long long *>(c->h_small.p + 64);
+    unsigned long long *hst = reinterpret_cast<unsigned long long *>(c->h_small.p + 128);
+    HIPCHK(hipMemcpyAsync(h, c->counters.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, ax));
+    HIPCHK(hipMemcpyAsync(hst, c->stats.p, sizeof(unsigned long long) * CCD_NSTATS, hipMemcpyDeviceToHost, ax));
+    if (c->done) HIPCHK(hipEventRecord(c->done, ax));
+    return 0;
+}
+
+static int finish(ccdgpu_ctx *c, double *kernel_seconds, bool *again) {
+    const ccdgpu_params &p = c->params;
+    const Shape &sh = c->shape;
+    const int nc = sh.n_chips();
+    hipStream_t ax = c->aux;
+    unsigned long long *h = reinterpret_cast<unsigned long long *>(c->h_small.p + 64);
+    unsigned long long *hst = reinterpret_cast<unsigned long long *>(c->h_small.p + 128);
+    *again = false;
+    if (c->done) {
+        HIPCHK(hipEventSynchronize(c->done));
+    } else {
+        HIPCHK(hipStreamSynchronize(ax));
+    }
+    if (h[4] >= 100000) {
+        // checking build: every call site that ran without a full EXEC, from the line bitmap
+        // (bit = line / 2) in stats[8 ..]
         const unsigned long long *st = hst;
-        for (int i = 0; i < CCD_NSTATS; ++i) c->diag[i] = st[i];
-        // CSR: exclusive scan of per-pixel counts, then scatter the pool
+        std::string lines;
+        for (int w = 8; w < CCD_NSTATS; ++w)
+            for (int b = 0; b < 64; ++b)
+                if ((st[w] >> b) & 1ull) {
+                    const int l0 = 2 * (64 * (w - 8) + b);
+                    lines += (lines.empty() ? "" : ", ") + std::to_string(l0) + "-" + std::to_string(l0 + 1);
+                }
+        return fail(CCDGPU_EHIP, "cross-lane primitive ran without a full EXEC at ccd_kernels.hip line " +
+                                     std::to_string(h[4] - 100000) + " (all call sites: lines " + lines + ")");
+    }
+    if (h[4]) return fail(CCDGPU_EHIP, "kernel index guard tripped at ccd_kernels.hip line " + std::to_string(h[4]));
+    if (h[3]) {  // pool overflow: grow and rerun
+        c->pool_cap = (int64_t)(h[1] + h[1] / 4 + 1024);
         int rc;
-        if ((rc = c->csr.ensure(c->n_pool > 0 ? c->n_pool : 1))) return rc;
-        size_t tmp_bytes = 0;
-        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, c->nseg.p, c->offsets.p, (int)c->total_pix + 1, ax));
-        if ((rc = c->cub_tmp.ensure(tmp_bytes))) return rc;
-        // nseg has total_pix entries; the scan over total_pix+1 needs a trailing zero
-        HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->cub_tmp.p, tmp_bytes, c->nseg.p, c->offsets.p, (int)c->total_pix, ax));
-        c->h_offsets.resize(c->total_pix + 1);
-        if ((rc = c->h_off.ensure(sizeof(int64_t) * (size_t)c->total_pix))) return rc;
-        HIPCHK(hipMemcpyAsync(c->h_off.p, c->offsets.p, sizeof(int64_t) * c->total_pix, hipMemcpyDeviceToHost, ax));
-        HIPCHK(hipStreamSynchronize(ax));
-        std::memcpy(c->h_offsets.data(), c->h_off.p, sizeof(int64_t) * (size_t)c->total_pix);
-        c->h_offsets[c->total_pix] = c->n_pool;
-        if (ccdk_scatter(c->pool.p, c->pool_seq.p, c->n_pool, c->offsets.p, c->chip_pix_off.p, nc, c->csr.p, ax))
-            return fail(CCDGPU_EHIP, "scatter launch failed");
-        HIPCHK(hipEventRecord(c->ev[3], ax));
-        HIPCHK(hipStreamSynchronize(ax));
-        c->last.detect_ms = ms_det;
-        c->last.detect_ms_device = h[6] > h[5] ? (double)(h[6] - h[5]) / 1e5 : 0.0;  // 100 MHz clock
-        c->last.prep_ms = ms_prep;
-        c->last.pixels = c->total_pix;
-        c->last.segments = c->n_pool;
-        c->last.lasso_fits = (int64_t)st[0];
-        c->last.cd_sweeps = (int64_t)st[1];
-        c->last.flops = (int64_t)st[2];
-        const int64_t in_bytes = sh.total_data() * 16 + sh.total_obs() * 8;
-        const int64_t out_bytes = c->n_pool * (int64_t)sizeof(ccdgpu_segment) + c->total_pix * ((int64_t)c->mask_words * 4 + 4 + 24 + 4);
-        c->last.bytes = in_bytes + out_bytes;
-        if (kernel_seconds) *kernel_seconds = (ms_prep + ms_det) * 1e-3;
-        c->ran = true;
-        if (h[7] != ~0ull)
-            return fail(CCDGPU_EOVERFLOW, "adaptive peek of pixel " + std::to_string(h[7]) + " exceeds " +
-                                              std::to_string(CCDGPU_MAX_PEEK) + " observations (PEEK_SIZE " +
-                                              std::to_string(p.peek_size) + ")");
-        if (h[2] != ~0ull) {
-            g_err = "unsupported bit-packed QA value (pixel " + std::to_string(h[2]) + ")";
-            return CCDGPU_EQA;
-        }
+        if ((rc = c->pool.ensure(c->pool_cap)) || (rc = c->pool_seq.ensure(c->pool_cap))) return rc;
+        *again = true;
         return 0;
+    }
+    c->n_pool = (int64_t)h[1];
+    float ms_prep = 0.f, ms_det = 0.f;
+    (void)hipEventElapsedTime(&ms_prep, c->ev[0], c->ev[1]);
+    (void)hipEventElapsedTime(&ms_det, c->ev[1], c->ev[2]);
+    const unsigned long long *st = hst;
+    for (int i = 0; i < CCD_NSTATS; ++i) c->diag[i] = st[i];
+    // CSR: exclusive scan of per-pixel counts, then scatter the pool
+    int rc;
+    if ((rc = c->csr.ensure(c->n_pool > 0 ? c->n_pool : 1))) return rc;
+    size_t tmp_bytes = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, c->nseg.p, c->offsets.p, (int)c->total_pix + 1, ax));
+    if ((rc = c->cub_tmp.ensure(tmp_bytes))) return rc;
+    // nseg has total_pix entries; the scan over total_pix+1 needs a trailing zero
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->cub_tmp.p, tmp_bytes, c->nseg.p, c->offsets.p, (int)c->total_pix, ax));
+    c->h_offsets.resize(c->total_pix + 1);
+    if ((rc = c->h_off.ensure(sizeof(int64_t) * (size_t)c->total_pix))) return rc;
+    HIPCHK(hipMemcpyAsync(c->h_off.p, c->offsets.p, sizeof(int64_t) * c->total_pix, hipMemcpyDeviceToHost, ax));
+    HIPCHK(hipStreamSynchronize(ax));
+    std::memcpy(c->h_offsets.data(), c->h_off.p, sizeof(int64_t) * (size_t)c->total_pix);
+    c->h_offsets[c->total_pix] = c->n_pool;
+    if (ccdk_scatter(c->pool.p, c->pool_seq.p, c->n_pool, c->offsets.p, c->chip_pix_off.p, nc, c->csr.p, ax))
+        return fail(CCDGPU_EHIP, "scatter launch failed");
+    HIPCHK(hipEventRecord(c->ev[3], ax));
+    HIPCHK(hipStreamSynchronize(ax));
+    c->last.detect_ms = ms_det;
+    c->last.detect_ms_device = h[6] > h[5] ? (double)(h[6] - h[5]) / 1e5 : 0.0;  // 100 MHz clock
+    c->last.prep_ms = ms_prep;
+    c->last.pixels = c->total_pix;
+    c->last.segments = c->n_pool;
+    c->last.lasso_fits = (int64_t)st[0];
+    c->last.cd_sweeps = (int64_t)st[1];
+    c->last.flops = (int64_t)st[2];
+    const int64_t in_bytes = sh.total_data() * 16 + sh.total_obs() * 8;
+    const int64_t out_bytes = c->n_pool * (int64_t)sizeof(ccdgpu_segment) + c->total_pix * ((int64_t)c->mask_words * 4 + 4 + 24 + 4);
+    c->last.bytes = in_bytes + out_bytes;
+    if (kernel_seconds) *kernel_seconds = (ms_prep + ms_det) * 1e-3;
+    c->ran = true;
+    if (h[7] != ~0ull)
+        return fail(CCDGPU_EOVERFLOW, "adaptive peek of pixel " + std::to_string(h[7]) + " exceeds " +
+                                          std::to_string(CCDGPU_MAX_PEEK) + " observations (PEEK_SIZE " +
+                                          std::to_string(p.peek_size) + ")");
+    if (h[2] != ~0ull) {
+        g_err = "unsupported bit-packed QA value (pixel " + std::to_string(h[2]) + ")";
+        return CCDGPU_EQA;
+    }
+    return 0;
+}
+
+int ccdgpu_run_staged(ccdgpu_ctx *c, double *kernel_seconds) {
+    if (!c || !c->staged) return fail(CCDGPU_EINVAL, "nothing staged");
+    if (c->pending) return fail(CCDGPU_EINVAL, "a detection begun with ccdgpu_run_slot_begin is not finished");
+    HIPCHK(hipSetDevice(c->device));
+    CcdDetectArgs a;
+    detect_args(c, a);
+    for (int attempt = 0; attempt < 4; ++attempt) {
+        int rc = launch(c, a);
+        if (rc) return rc;
+        bool again = false;
+        rc = finish(c, kernel_seconds, &again);
+        if (!again) return rc;
     }
     return fail(CCDGPU_EOVERFLOW, "segment pool kept overflowing");
 }

@@ -95,3 +95,37 @@ class OracleContext(object):
 
     def close(self):
         pass
+
+
+class SplitOracleContext(OracleContext):
+    """OracleContext with the device context's split run (run_slot_begin / run_done /
+    run_slot_end): the detection "runs" for ``run_time`` seconds after begin, during which the
+    runner stages the batches its fetch thread finishes into other slots."""
+
+    def __init__(self, device=0, threads=2, run_time=0.05, **kw):
+        super(SplitOracleContext, self).__init__(device, threads, **kw)
+        self.run_time = run_time
+        self._pending = None
+        self.staged_during_run = 0
+
+    def stage_slot_chips(self, slot, batch, params=None):
+        if self._pending is not None:
+            assert slot != self._pending[0], 'staged into the slot being detected'
+            self.staged_during_run += 1
+        super(SplitOracleContext, self).stage_slot_chips(slot, batch, params)
+
+    def run_slot_begin(self, slot):
+        import time
+        assert self._pending is None, 'run_slot_begin twice'
+        assert slot in self._slots, 'slot has no staged batch'
+        self._pending = (slot, time.perf_counter() + self.run_time)
+
+    def run_done(self):
+        import time
+        return self._pending is None or time.perf_counter() >= self._pending[1]
+
+    def run_slot_end(self):
+        slot, _ = self._pending
+        self._pending = None
+        self.run_slot(slot)
+

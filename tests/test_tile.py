@@ -59,6 +59,28 @@ def test_single_process_tile_run():
     assert (rows['py'][off[:-1]] == cy).all() and mask.shape == (N_PIX, res['chips'][4]['n_obs'])
 
 
+def test_tile_run_stages_uploads_while_a_detection_runs():
+    """With a context that runs detections asynchronously (run_slot_begin / run_done /
+    run_slot_end, as ccdgpu.Context), the worker uploads the batches its fetch thread finishes
+    while a detection runs, never into the running slot, and the rows are those of the plain
+    synchronous run."""
+    from ccdc import runner
+    from rows_util import OracleContext, SplitOracleContext
+    made = []
+
+    def split(dev):
+        made.append(SplitOracleContext(dev, threads=2, run_time=0.2))
+        return made[-1]
+
+    sink = runner.SummarySink(keep_rows=True)
+    res = runner.changedetection(tile(), source, contexts=2, batch_chips=1, number=N_CHIPS, sink=sink,
+                                 context_factory=split)
+    ref = runner.changedetection(tile(), source, contexts=1, batch_chips=3, number=N_CHIPS,
+                                 context_factory=lambda dev: OracleContext(dev, threads=2))
+    assert [c['digest'] for c in res['chips']] == [c['digest'] for c in ref['chips']]
+    assert sum(c.staged_during_run for c in made) > 0
+
+
 def _free_port():
     s = socket.socket()
     s.bind(('127.0.0.1', 0))
