@@ -274,6 +274,14 @@ int ccdgpu_fetch_rows(ccdgpu_ctx *ctx, int32_t chip, int32_t cx, int32_t cy, int
  * back bit-packed (out->mask_bits [n_pix of the batch][out->mask_words], out->mask NULL);
  * out->n_obs is 0 for a multi-chip batch. */
 int ccdgpu_fetch_batch_rows(ccdgpu_ctx *ctx, const int32_t *cx, const int32_t *cy, int32_t width, ccdgpu_rows *out);
+/* ccdgpu_fetch_batch_rows into the caller's buffers (no library allocation, no host copy of the
+ * rows or mask words: with pinned buffers from ccdgpu_host_alloc they arrive by DMA):
+ * row_offsets [total_pixels + 1], rows [*n_rows], mask_bits [total_pixels][mask_words].  The
+ * row count is set in *n_rows even when a buffer is too small (CCDGPU_EINVAL, nothing fetched:
+ * grow and call again).  The tile driver reuses one set of pinned buffers per context. */
+int ccdgpu_fetch_batch_rows_into(ccdgpu_ctx *ctx, const int32_t *cx, const int32_t *cy, int32_t width,
+                                 int64_t *row_offsets, int64_t offsets_cap, ccdgpu_row *rows, int64_t rows_cap,
+                                 uint32_t *mask_bits, int64_t mask_cap, int64_t *n_rows);
 void ccdgpu_rows_free(ccdgpu_rows *out);
 
 /* Kernel statistics of the last run (per launch of the main detection kernel). */

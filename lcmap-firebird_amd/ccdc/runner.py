@@ -333,6 +333,10 @@ def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, er
         free = list(range(depth + 1))
         staged = []  # (slot, positions, batch), in upload order
         split = hasattr(ctx, 'run_slot_begin')  # (test doubles have run_slot only)
+        into = None  # the context's reusable pinned landing buffers for the rows
+        if hasattr(ctx, 'fetch_batch_rows_into'):
+            import ccdgpu
+            into = ccdgpu.RowsBuffers()
         exhausted = False
         while True:
             while free and not exhausted:
@@ -387,7 +391,10 @@ def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, er
             t3 = clock()
             cx = np.array([xys[p][0] for p in ppos], dtype=np.int32)
             cy = np.array([xys[p][1] for p in ppos], dtype=np.int32)
-            off, rows, mask = ctx.fetch_batch_rows(cx, cy, width)
+            if into is not None:  # views of the landing buffers: valid until the next batch's fetch
+                off, rows, mask = ctx.fetch_batch_rows_into(cx, cy, into, width)
+            else:
+                off, rows, mask = ctx.fetch_batch_rows(cx, cy, width)
             free.append(s)  # its rows are fetched: the slot takes the next upload
             permits.release()
             t4 = clock()
@@ -431,7 +438,8 @@ def detect_tile(xys, source, queue, device=0, contexts=4, batch_chips=8, params=
     gets each batch back once its rows are fetched, to reuse its buffers); ``queue`` hands out positions (LocalQueue
     for one process, StoreQueue across ranks); ``sink(pos, cx, cy, dates, row_offsets, rows,
     mask_bits)`` receives each chip's device-packed rows and its processing masks as bit words
-    [n_pix][words] (ccdgpu.abi.unpack_mask_bits; default sink: a SummarySink).  Returns the sink
+    [n_pix][words] (ccdgpu.abi.unpack_mask_bits; default sink: a SummarySink) -- views of the
+    context's reusable landing buffers, valid during the call: a sink that keeps them copies.  Returns the sink
     and this process's statistics.  ``upload_depth``: batches each context keeps uploaded or
     uploading ahead of the one it detects (1 .. ccdgpu.UPLOAD_SLOTS - 1).  ``tail_chips``: once
     fewer positions than this remain in the queue, workers pull quarter batches (default: two

@@ -38,6 +38,10 @@ def _declare(L):
     L.ccdgpu_last_error.restype = c.c_char_p
     L.ccdgpu_params_default.argtypes = [c.POINTER(abi.Params)]
     L.ccdgpu_init.argtypes = [c.c_int, c.POINTER(c.c_void_p)]
+    if hasattr(L, 'ccdgpu_fetch_batch_rows_into'):
+        L.ccdgpu_fetch_batch_rows_into.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_int32, c.c_void_p, c.c_int64,
+                                                   c.c_void_p, c.c_int64, c.c_void_p, c.c_int64, c.POINTER(c.c_int64)]
+        L.ccdgpu_fetch_batch_rows_into.restype = c.c_int
     if hasattr(L, 'ccdgpu_run_slot_begin'):
         L.ccdgpu_run_slot_begin.argtypes = [c.c_void_p, c.c_int32]
         L.ccdgpu_run_slot_begin.restype = c.c_int
@@ -107,7 +111,7 @@ EXPORTS = ('ccdgpu_version', 'ccdgpu_last_error', 'ccdgpu_params_default', 'ccdg
            'ccdgpu_last_stats', 'ccdgpu_diag_counters', 'ccdgpu_stage_chips', 'ccdgpu_stage_slot_chips',
            'ccdgpu_fetch_batch_rows', 'ccdgpu_device_numa_node', 'ccdgpu_encoded_bound', 'ccdgpu_encode_chips',
            'ccdgpu_encode_vector_path', 'ccdgpu_stage_slot_encoded', 'ccdgpu_init_copy_cus',
-           'ccdgpu_run_slot_begin', 'ccdgpu_run_query', 'ccdgpu_run_slot_end')
+           'ccdgpu_run_slot_begin', 'ccdgpu_run_query', 'ccdgpu_run_slot_end', 'ccdgpu_fetch_batch_rows_into')
 
 
 def lib():
@@ -484,6 +488,37 @@ class Context(object):
         finally:
             lib().ccdgpu_rows_free(ctypes.byref(r))
 
+    def fetch_batch_rows_into(self, cx, cy, bufs, width=100):
+        """fetch_batch_rows into ``bufs`` (a RowsBuffers, reused across batches: pinned, so the
+        rows and mask words arrive by DMA with no host copy; ccdgpu_fetch_batch_rows_into).
+        Returns views of its arrays, valid until its next use."""
+        batch = self._keep
+        if not isinstance(batch, ChipBatch):
+            raise ValueError('fetch_batch_rows needs a stage_chips / stage_slot_chips batch')
+        cx = np.ascontiguousarray(cx, dtype=np.int32)
+        cy = np.ascontiguousarray(cy, dtype=np.int32)
+        if cx.shape != (batch.n_chips,) or cy.shape != (batch.n_chips,):
+            raise ValueError('cx / cy need one entry per chip (%d)' % batch.n_chips)
+        L = lib()
+        if not hasattr(L, 'ccdgpu_fetch_batch_rows_into'):  # (libraries built before it: A/B runs)
+            return self.fetch_batch_rows(cx, cy, width)
+        n_pix = int(batch.pix_off[-1])
+        words = (int(batch.n_obs.max()) + 31) // 32
+        bufs.ensure(n_pix + 1, n_pix * 2, n_pix * words)
+        nr = ctypes.c_int64(0)
+        for _ in range(2):
+            rc = L.ccdgpu_fetch_batch_rows_into(self._ctx, cx.ctypes.data, cy.ctypes.data, int(width),
+                                                bufs.offsets.ctypes.data, bufs.offsets.size, bufs.rows.ctypes.data,
+                                                bufs.rows.size, bufs.mask.ctypes.data, bufs.mask.size, ctypes.byref(nr))
+            if rc == 0:
+                break
+            if rc != abi.E_INVAL or nr.value <= bufs.rows.size:
+                _check(rc)
+            bufs.ensure(n_pix + 1, nr.value, n_pix * words)  # more rows than the first guess
+        else:
+            _check(rc)
+        return bufs.offsets[:n_pix + 1], bufs.rows[:nr.value], bufs.mask[:n_pix * words].reshape(n_pix, words)
+
     def stage_slot(self, slot, dates, spectra, qa, params=None):
         """Upload a batch into input slot 0 .. UPLOAD_SLOTS-1 on the copy stream and return at once (the arrays
         must stay alive and unchanged until run_slot(slot) returns; pinned arrays from
@@ -635,6 +670,28 @@ def batch_storage(max_chips, max_pix, max_obs, pinned=True):
     alloc = pinned_empty if pinned else np.empty
     n = int(max_chips) * int(max_pix) * int(max_obs)
     return (alloc((int(max_chips) * int(max_obs),), np.int64), alloc((7 * n,), np.int16), alloc((n,), np.uint16))
+
+
+class RowsBuffers(object):
+    """Reusable (pinned) landing buffers of Context.fetch_batch_rows_into: row offsets, rows
+    (abi.ROW_DTYPE) and mask words; grown on demand, 25 % headroom."""
+
+    def __init__(self, pinned=True):
+        self.pinned = pinned
+        self.offsets = np.zeros(0, np.int64)
+        self.rows = np.zeros(0, abi.ROW_DTYPE)
+        self.mask = np.zeros(0, np.uint32)
+
+    def _grow(self, arr, n, dtype):
+        if arr.size >= n:
+            return arr
+        n = int(n * 1.25) + 64
+        return pinned_empty((n,), dtype) if self.pinned else np.empty(n, dtype)
+
+    def ensure(self, n_offsets, n_rows, n_words):
+        self.offsets = self._grow(self.offsets, n_offsets, np.int64)
+        self.rows = self._grow(self.rows, n_rows, abi.ROW_DTYPE)
+        self.mask = self._grow(self.mask, n_words, np.uint32)
 
 
 def pinned_empty(shape, dtype):

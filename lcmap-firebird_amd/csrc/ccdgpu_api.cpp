@@ -1090,6 +1090,52 @@ int ccdgpu_fetch_batch_rows(ccdgpu_ctx *c, const int32_t *cx, const int32_t *cy,
     return fetch_rows_range(c, 0, c->shape.n_chips(), cx, cy, width, out, true);
 }
 
+int ccdgpu_fetch_batch_rows_into(ccdgpu_ctx *c, const int32_t *cx, const int32_t *cy, int32_t width, int64_t *row_offsets,
+                                 int64_t offsets_cap, ccdgpu_row *rows, int64_t rows_cap, uint32_t *mask_bits,
+                                 int64_t mask_cap, int64_t *n_rows) {
+    if (!c || !cx || !cy || !row_offsets || !rows || !mask_bits || !n_rows) return fail(CCDGPU_EINVAL, "NULL argument");
+    *n_rows = 0;
+    if (!c->ran || c->shape.n_chips() <= 0) return fail(CCDGPU_EINVAL, "no completed run to fetch");
+    if (width <= 0) return fail(CCDGPU_EINVAL, "width must be > 0");
+    HIPCHK(hipSetDevice(c->device));
+    const Shape &sh = c->shape;
+    const int32_t nc = sh.n_chips();
+    const int64_t np = sh.pix_off[nc];
+    // rows per pixel = max(1, segments), from the segment offsets already on the host
+    int64_t nr = 0;
+    for (int64_t i = 0; i < np; ++i) nr += std::max<int64_t>(1, c->h_offsets[i + 1] - c->h_offsets[i]);
+    *n_rows = nr;
+    const size_t nbits = (size_t)np * c->mask_words;
+    if (offsets_cap < np + 1 || rows_cap < nr || mask_cap < (int64_t)nbits)
+        return fail(CCDGPU_EINVAL, "fetch_batch_rows_into: buffers too small (need " + std::to_string(np + 1) +
+                                       " offsets, " + std::to_string(nr) + " rows, " + std::to_string(nbits) + " mask words)");
+    int rc;
+    if ((rc = c->rows.ensure((size_t)(nr > 0 ? nr : 1))) || (rc = c->row_off.ensure(np + 1)) || (rc = c->seg_off1.ensure(np + 1)))
+        return rc;
+    const size_t ob = sizeof(int64_t) * (size_t)(np + 1);
+    if ((rc = c->h_fo.ensure(2 * ob))) return rc;
+    int64_t *soff = reinterpret_cast<int64_t *>(c->h_fo.p), *roff = soff + (np + 1);
+    const int64_t s0 = c->h_offsets[0];
+    roff[0] = 0;
+    for (int64_t i = 0; i <= np; ++i) soff[i] = c->h_offsets[i] - s0;
+    for (int64_t i = 0; i < np; ++i) roff[i + 1] = roff[i] + std::max<int64_t>(1, soff[i + 1] - soff[i]);
+    hipStream_t ax = c->aux;
+    HIPCHK(hipMemcpyAsync(c->seg_off1.p, soff, ob, hipMemcpyHostToDevice, ax));
+    HIPCHK(hipMemcpyAsync(c->row_off.p, roff, ob, hipMemcpyHostToDevice, ax));
+    for (int32_t ch = 0; ch < nc; ++ch) {
+        const int64_t q = sh.pix_off[ch];
+        if (ccdk_pack_rows(c->csr.p + s0, c->seg_off1.p + q, c->row_off.p + q, c->mask.p + (size_t)q * c->mask_words,
+                           c->mask_words, sh.npix[ch], sh.nobs[ch], cx[ch], cy[ch], width, c->rows.p, nullptr, ax))
+            return fail(CCDGPU_EHIP, "row packing launch failed");
+    }
+    // straight into the caller's buffers (DMA when they are pinned: ccdgpu_host_alloc)
+    if (nr > 0) HIPCHK(hipMemcpyAsync(rows, c->rows.p, sizeof(ccdgpu_row) * (size_t)nr, hipMemcpyDeviceToHost, ax));
+    if (nbits > 0) HIPCHK(hipMemcpyAsync(mask_bits, c->mask.p, sizeof(uint32_t) * nbits, hipMemcpyDeviceToHost, ax));
+    std::memcpy(row_offsets, roff, ob);
+    HIPCHK(hipStreamSynchronize(ax));
+    return 0;
+}
+
 void ccdgpu_rows_free(ccdgpu_rows *r) {
     if (!r) return;
     std::free(r->row_offsets);

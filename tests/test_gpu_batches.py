@@ -89,6 +89,36 @@ def test_batch_rows_equal_per_chip_rows(ctx):
         assert np.array_equal(off[p0:p1 + 1] - off[p0], o1)
         assert rows[off[p0]:off[p1]].tobytes() == r1.tobytes()
         assert np.array_equal(batch.mask_of(mask, c), m1)
+    # the same rows into reusable pinned buffers (ccdgpu_fetch_batch_rows_into), including a
+    # first guess of the row count that is too small
+    bufs = ccdgpu.RowsBuffers()
+    bufs.ensure(1, 1, 1)
+    for _ in range(2):
+        o2, r2, m2 = ctx.fetch_batch_rows_into(cx, cy, bufs)
+        assert np.array_equal(o2, off) and r2.tobytes() == rows.tobytes() and np.array_equal(m2, mask)
+
+
+def test_split_run_equals_run_slot(ctx):
+    """ccdgpu_run_slot_begin / _query / _end give what ccdgpu_run_slot gives, with another slot
+    staged while the detection runs; a second begin before the end is refused."""
+    chips = tile_mix(200)
+    b = ccdgpu.ChipBatch.from_chips(chips, pinned=True)
+    ctx.stage_slot_chips(0, b)
+    ctx.run_slot(0)
+    ref = [ctx.fetch(i) for i in range(len(chips))]
+    ctx.stage_slot_chips(0, b)
+    ctx.run_slot_begin(0)
+    ctx.stage_slot_chips(1, b)
+    with pytest.raises(ccdgpu.CcdGpuError):
+        ctx.run_slot_begin(1)
+    while not ctx.run_done():
+        pass
+    ctx.run_slot_end()
+    for i in range(len(chips)):
+        g = ctx.fetch(i)
+        assert g.segments.tobytes() == ref[i].segments.tobytes() and np.array_equal(g.mask, ref[i].mask)
+    ctx.run_slot(1)
+    assert ctx.fetch(0).segments.tobytes() == ref[0].segments.tobytes()
 
 
 def test_slots_keep_their_own_params(ctx):

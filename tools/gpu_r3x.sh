@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round-3 GPU call X: workers stage uploads while their detection runs (ccdgpu_run_slot_begin /
+# Round-3 GPU call X: rows fetched into reusable pinned buffers; workers stage uploads while their
+# detection runs (ccdgpu_run_slot_begin /
 # _query / _end): GPU suite, tile runs (4x3 default twice, 4x4, 6x2), kernel + copy timeline.
 set -o pipefail
 R=$(pwd); O=$R/gpurun_out/r03x; mkdir -p $O
