@@ -89,10 +89,9 @@ def test_batch_rows_equal_per_chip_rows(ctx):
         assert np.array_equal(off[p0:p1 + 1] - off[p0], o1)
         assert rows[off[p0]:off[p1]].tobytes() == r1.tobytes()
         assert np.array_equal(batch.mask_of(mask, c), m1)
-    # the same rows into reusable pinned buffers (ccdgpu_fetch_batch_rows_into), including a
-    # first guess of the row count that is too small
+    # the same rows into reusable pinned buffers (ccdgpu_fetch_batch_rows_into), twice into the
+    # same buffers
     bufs = ccdgpu.RowsBuffers()
-    bufs.ensure(1, 1, 1)
     for _ in range(2):
         o2, r2, m2 = ctx.fetch_batch_rows_into(cx, cy, bufs)
         assert np.array_equal(o2, off) and r2.tobytes() == rows.tobytes() and np.array_equal(m2, mask)
