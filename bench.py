@@ -87,6 +87,16 @@ def parse():
                     help='tile leg transport encoding: drop the band values of fill/cloud/shadow observations '
                          '(never read by the detection; default) or only of fill observations (lossless)')
     ap.add_argument('--tile-depth', type=int, default=2, help='batches each tile-leg context keeps uploaded ahead')
+    ap.add_argument('--tile-split', action='store_true',
+                    help='the north-star mode: ONE 2500-chip tile split over all ranks through the shared queue '
+                         '(strong scaling; value = the tile\'s pixels / its wall time) instead of one tile per rank')
+    ap.add_argument('--no-north-star', action='store_true',
+                    help='N > 1: skip the extra one-tile-over-all-ranks run reported as north_star_tile')
+    ap.add_argument('--tile-parity-pixels', type=int, default=1,
+                    help='pixels per tile position re-detected by the C oracle after the timed tile run '
+                         '(tile.parity_sample; 0 = none)')
+    ap.add_argument('--roofline-launches', type=int, default=3,
+                    help='single-context launches of the resident batch timed for the roofline (per-launch duration)')
     ap.add_argument('--share-device', action='store_true',
                     help='rehearsal only: ranks beyond the device count share devices (LOCAL_RANK mod count)')
     return ap.parse_args()
@@ -203,7 +213,14 @@ def main():
         if dist is not None:
             dist.destroy_process_group()
         return
-    tl = tile_leg(args, cfg, rank, world, device, dist)
+    tl = tile_leg(args, cfg, rank, world, device, dist, split=args.tile_split)
+    north = None
+    if world > 1 and not args.tile_split and not args.no_north_star:
+        # the north-star target: one tile over all ranks (BASELINE.json north_star; core.py:97-108)
+        import copy
+        a3 = copy.copy(args)
+        a3.warmup = 0
+        north = tile_leg(a3, cfg, rank, world, device, dist, split=True)
     tl_lossless = None
     if not args.no_tile_lossless and not args.tile_no_encode and args.tile_encode != 'lossless':
         # the same tile with the lossless encoding (device inputs bit-identical to the raw chips)
@@ -221,23 +238,26 @@ def main():
             'warmup': args.warmup,
             'ms_per_step': tl['ms_per_step'],
             'higher_is_better': True,
-            'scaling': 'weak',
+            'scaling': 'strong' if args.tile_split else 'weak',
             'vs_baseline': None,
             'dtype': 'f64',
             'data': 'synthetic (Landsat 4-8 ARD, seeded; tile leg: every chip distinct -- date-shifted copies of GPU-generated pool chips)',
             'config': {
-                'workload': '%s; one full 5000x5000-pixel tile per GPU (%d distinct 100x100-pixel chips per rank, %s), '
+                'workload': '%s; %s (%d distinct 100x100-pixel chips per rank, %s), '
                             'PCIe-inclusive: chips uploaded from pinned host memory in the runner\'s transport encoding '
                             '(%s), detected, segment/pixel rows packed '
                             'on the device and fetched back, per-chip summaries gathered on rank 0 (ccdc.runner.changedetection); '
                             'a step = %d chips per rank' % (
-                                CONFIG_NAMES[args.config], tl['chips_per_rank'],
+                                CONFIG_NAMES[args.config],
+                                'ONE full 5000x5000-pixel tile split over all %d GPUs' % world if args.tile_split
+                                else 'one full 5000x5000-pixel tile per GPU', tl['chips_per_rank'],
                                 ', '.join('%d chips of %d obs' % (v, k) for k, v in sorted(tl['n_obs_mix'].items())),
                                 'raw upload' if args.tile_no_encode else
                                 'band values of fill/cloud/shadow observations, which the detection never reads, not sent'
                                 if args.tile_encode == 'unread' else 'lossless',
                                 tl['chips_per_step']),
-                'workload_key': 'tile%d_config%d_chips%d_pcie' % (args.tile_chips, args.config, tl['chips_per_rank']),
+                'workload_key': 'tile%d_config%d_chips%d_pcie%s' % (args.tile_chips, args.config, tl['chips_per_rank'],
+                                                                   '_split' if args.tile_split else ''),
                 'synthetic_config': args.config,
                 'chips_per_gpu': tl['chips_per_rank'],
                 'pixels_per_chip': PIXELS_PER_CHIP,
@@ -245,12 +265,19 @@ def main():
                 'tile_chips': TILE_CHIPS,
                 'ranks': world,
                 'parallelism': 'chip-sharded x%d (one process per GPU, shared dynamic chip queue, no collective)' % world,
+                'tile_split': bool(args.tile_split),
             },
             'roofline': res['roofline'],
             'value_resident': res['value'],
             'resident': res,
             'tile': tl,
         }
+        if north is not None:
+            out['north_star_tile'] = {k: north.get(k) for k in (
+                'value', 'unit', 'seconds', 'chips', 'pixels', 'chips_per_rank_done', 'tail_seconds_per_rank',
+                'parity_sample')}
+            out['north_star_tile']['note'] = ('one 2500-chip tile split over all %d ranks through the shared queue '
+                                              '(strong scaling; the target of BASELINE.json north_star)' % world)
         if tl_lossless is not None:
             out['tile_lossless'] = {k: tl_lossless[k] for k in ('value', 'unit', 'seconds', 'transport_encoding',
                                                                  'worker_seconds_rank0')}
@@ -324,15 +351,24 @@ def resident_leg(args, cfg, rank, world, device, dist, batch=None):
     barrier()
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed, dist)
+    det_avg = float(np.mean(det_ms))
+    dev_avg = float(np.mean(dev_ms))
+    # per-launch time behind the roofline: launches of ONE context, back to back, nothing else on
+    # the device -- the HIP-event duration of each detection launch on the stream it is launched
+    # on, averaged (= rocprofv3's average dispatch duration of a single-context run:
+    # profiles/<round>/kernel_stats*.csv).  With two contexts a launch overlaps the other's tail
+    # and its duration is inflated, so the timed steps above are not used for it.
+    rl_ms, rl_dev = [], []
+    for _ in range(max(1, args.roofline_launches)):
+        ctx.run()
+        st = ctx.stats()
+        rl_ms.append(st['detect_ms'])
+        rl_dev.append(st['detect_ms_device'])
+        flops = st['flops']
     for c in ctxs:
         c.close()
     value = world * batch.total_pixels * args.steps / elapsed
-    det_avg = float(np.mean(det_ms))
-    dev_avg = float(np.mean(dev_ms))
-    # per-launch time behind the roofline: the HIP-event launch duration on the launching stream;
-    # with concurrent contexts a launch can queue behind the other context's kernel (counted by
-    # its events), so there the kernel's own execution window on the device clock is used
-    launch_ms = det_avg if len(ctxs) == 1 else dev_avg
+    launch_ms = float(np.mean(rl_ms))
     achieved_tf = flops / (launch_ms * 1e-3) / 1e12
     mix = cadence_mix(batch)
     workload_key = 'config%d_chips%d_mix%s' % (args.config, len(ids), '-'.join('%dx%d' % (k, v) for k, v in sorted(mix.items())))
@@ -365,8 +401,11 @@ def resident_leg(args, cfg, rank, world, device, dist, batch=None):
             'workload_key': workload_key,
             'traffic_note': 'traffic = HBM bytes per launch from rocprofv3 --pmc (profiles/pmc_detect.json, same workload_key), else null',
             'kernel_ms_per_launch': launch_ms,
-            'kernel_ms_hip_events': det_avg,
-            'kernel_ms_device_clock': dev_avg,
+            'kernel_ms_per_launch_note': 'mean HIP-event duration of %d single-context launches (launching stream)' % len(rl_ms),
+            'kernel_ms_single_context_launches': [round(x, 3) for x in rl_ms],
+            'kernel_ms_single_context_device_clock': float(np.mean(rl_dev)),
+            'kernel_ms_hip_events_timed_steps': det_avg,
+            'kernel_ms_device_clock_timed_steps': dev_avg,
             'wall_ms_per_launch': elapsed * 1e3 / args.steps,
             'flops_per_launch': flops,
             'algorithmic_bytes_per_launch': alg_bytes,
@@ -433,21 +472,25 @@ class _KeptContext(object):
         pass
 
 
-def tile_leg(args, cfg, rank, world, device, dist):
+def tile_leg(args, cfg, rank, world, device, dist, split=False):
     """The headline: ``--tile-chips`` distinct chips per rank (default one full 2500-chip tile)
     through ccdc.runner.changedetection with chips generated on the GPU into pinned host memory
     (ccdgpu.synth.TileSource).  Positions 0 .. world * tile_chips - 1 share one dynamic queue;
     position p is generator chip p (tile p // 2500, chip p % 2500 of it; coordinates on the
     reference grid of test/data/tile_response.json shifted one tile width per tile).  W warmup
-    steps run first on chips of a separate tile range (positions offset by 10^6)."""
+    steps run first on chips of a separate tile range (positions offset by 10^6).  ``split``: the
+    north-star mode -- ONE tile of ``--tile-chips`` positions over all ranks (strong scaling).
+    After the timed run, ``--tile-parity-pixels`` pixels of every position are re-detected by the
+    C oracle from the position's raw inputs (tests/tile_sample.py; the checker, outside the timing)
+    and reported as ``parity_sample``."""
     import ccdgpu
     from ccdc import runner
     from ccdgpu import synth
     B = args.tile_batch
     K = max(1, args.steps)
-    per_rank = int(args.tile_chips)
+    total = int(args.tile_chips) if split else world * int(args.tile_chips)
+    per_rank = -(-total // world)
     chips_per_step = -(-per_rank // K)
-    total = world * per_rank
     warm_total = world * min(per_rank, args.warmup * chips_per_step)
     # distinct chips: a pool of generated chips, each position a different rotation of one of them
     # (configs 3 / 5, whose chips share two date vectors); configs 2 / 4 subsample dates per chip,
@@ -486,10 +529,18 @@ def tile_leg(args, cfg, rank, world, device, dist):
         t, c = divmod(p % 1000000, TILE_CHIPS)
         return (-1815585 + 3000 * (c // 50) + 150000 * t, 1064805 - 3000 * (c % 50))
 
-    def run(n, src):
+    sample_sink = [None]
+
+    def run(n, src, sample=False):
         nonlocal lent
         lent = iter(ctxs)
         sink = runner.SummarySink(digest=False)
+        if sample and args.tile_parity_pixels > 0:
+            sys.path.insert(0, os.path.join(ROOT, 'tests'))
+            import tile_sample
+            k = int(args.tile_parity_pixels)
+            sink = sample_sink[0] = tile_sample.PixelSampleSink(
+                lambda pos: sorted({(int(pos) * 7919 + 13 + j * 1009) % PIXELS_PER_CHIP for j in range(k)}), sink)
         xys = [xy(p) for p in range(n)]
         # (encode=False: the source is already the encoding wrapper when the leg encodes)
         return runner.changedetection(xys, src, device=device, contexts=args.tile_contexts, batch_chips=B,
@@ -505,11 +556,14 @@ def tile_leg(args, cfg, rank, world, device, dist):
     enc0 = (esrc.bytes_raw, esrc.bytes_sent, esrc.encode_seconds) if encode else (0, 0, 0.0)
     cg0 = _cgroup_cpu()
     t = time.perf_counter()
-    res = run(total, src_timed)
+    res = run(total, src_timed, sample=True)
     ctxs[0].synchronize()
     if dist is not None:
         dist.barrier()
     el = max_over_ranks(time.perf_counter() - t, dist)
+    parity = None
+    if sample_sink[0] is not None:
+        parity = tile_parity_sample(sample_sink[0], src, cfg, mode, dist)
     gen_s = src.generate_seconds - gen0
     cg1 = _cgroup_cpu()
     cg = None
@@ -535,6 +589,7 @@ def tile_leg(args, cfg, rank, world, device, dist):
         mix[c['n_obs']] = mix.get(c['n_obs'], 0) + 1
     ranks = {st['rank']: st for st in res['ranks']}
     return {'value': px / el, 'unit': 'pixels/s', 'seconds': el, 'ms_per_step': el / K * 1e3, 'steps': K,
+            'split': bool(split), 'parity_sample': parity,
             'chips_per_step': chips_per_step, 'chips_per_rank': per_rank, 'chips': len(res['chips']), 'pixels': px,
             'distinct_chips': len(res['chips']), 'chips_per_launch': B, 'contexts_per_gpu': args.tile_contexts,
             'upload_depth': args.tile_depth, 'ranks': world, 'n_obs_mix': mix,
@@ -561,6 +616,39 @@ def tile_leg(args, cfg, rank, world, device, dist):
                                             'never read by the detection, results identical'
                                             if args.tile_encode == 'unread' else 'lossless')
                     if encode else 'chips copied into pinned batches by the runner\'s fetch threads, uploaded raw')}
+
+
+def tile_parity_sample(sink, src, cfg, mode, dist):
+    """Checker, after the timed tile run: the sampled pixels of every position this rank
+    detected, re-detected by the C oracle from the position's raw inputs (pool mode: the
+    position's moved dates and the pool chip's ARD; generate mode: the generator's pixels) and
+    compared row for row (tests/tile_sample.py); summed over ranks."""
+    sys.path.insert(0, os.path.join(ROOT, 'tests'))
+    import tile_sample
+    from ccdgpu import synth
+
+    def inputs(pos, pixels):
+        if mode == 'pool':
+            d, sp, q = src.views([pos])[0]
+            return d, sp[:, pixels], q[pixels]
+        parts = [synth.chip(cfg, int(pos), px, 1) for px in pixels]
+        return (parts[0][0], np.concatenate([p[1] for p in parts], axis=1),
+                np.concatenate([p[2] for p in parts], axis=0))
+
+    thr, _ = host_cpus()
+    t = time.perf_counter()
+    out = tile_sample.check(sink, inputs, threads=thr)
+    out['oracle_seconds_rank0'] = round(time.perf_counter() - t, 2)
+    if dist is not None:
+        import torch
+        v = torch.tensor([out['pixels'], out['chips'], out['int_mismatches'], out['float_mismatches']], dtype=torch.float64)
+        dist.all_reduce(v)
+        m = torch.tensor([out['max_rel']], dtype=torch.float64)
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        out.update(pixels=int(v[0]), chips=int(v[1]), int_mismatches=int(v[2]), float_mismatches=int(v[3]),
+                   max_rel=float(m[0]))
+    out['checker'] = 'C restatement oracle (oracle/libccdoracle.so), 1 thread per position, %d threads' % thr
+    return out
 
 
 def synth_nobs(cfg, c):
@@ -681,11 +769,15 @@ def restatement_baseline(dates, S, Q, args):
     n = min(args.restatement_pixels, S.shape[1])
     jobs = [(dates, S[:, p].copy(), Q[p].copy()) for p in range(n)]
     ctx = multiprocessing.get_context('spawn')
-    with ctx.Pool(thr) as pool:
+    pool = ctx.Pool(thr)
+    try:
         pool.map(_restatement_pixel, jobs[:thr])  # worker start-up and imports outside the timing
         t = time.perf_counter()
         pool.map(_restatement_pixel, jobs, chunksize=1)
         el = time.perf_counter() - t
+    finally:
+        pool.close()  # workers exit on their own (no terminate), then are reaped
+        pool.join()
     out = {'value': n / el, 'unit': 'pixels/s', 'cores': thr, 'kind': 'port',
            'label': 'pyccd-equivalent restatement (not pyccd itself)',
            'sample': 'first %d pixels of chip 0 of the same workload (%d obs, %.1f s), oracle/ccd_ref.py, multiprocessing.Pool(%d)' % (
@@ -694,5 +786,18 @@ def restatement_baseline(dates, S, Q, args):
     return out
 
 
+def _stop_helpers():
+    """End the multiprocessing resource tracker the spawn pool started (it would otherwise
+    outlive the JSON line as a stray process)."""
+    try:
+        from multiprocessing import resource_tracker
+        resource_tracker._resource_tracker._stop()
+    except Exception:
+        pass
+
+
 if __name__ == '__main__':
-    main()
+    try:
+        main()
+    finally:
+        _stop_helpers()

@@ -59,14 +59,14 @@ int64_t ccdgpu_encoded_bound(int32_t n_chips, const int32_t *n_pix, const int32_
 
 /* ---- band compaction: dst[k++] = src[i] for the observations kept (keep[i] = 1); *bad is set
  * when a dropped observation that must hold the fill value (strict[i] = 1) holds another one
- * (the chip then goes raw) */
+ * (the chip then goes raw).  Only kept values are written: dst has room for exactly this pixel's
+ * kept run, and the next pixel's run (another thread's, under the static schedule) follows it. */
 static size_t compact_scalar(const int16_t *src, const uint8_t *keep, const uint8_t *strict, int n, int16_t *dst,
                              int *bad) {
     size_t k = 0;
     int b = 0;
     for (int i = 0; i < n; ++i) {
-        dst[k] = src[i];
-        k += keep[i];
+        if (keep[i]) dst[k++] = src[i];
         b |= strict[i] & (src[i] != -9999);
     }
     *bad |= b;
@@ -409,7 +409,7 @@ static size_t encode_chip(int32_t n_pix, int32_t n_obs, const int16_t *spectra, 
             ret = encode_raw(n_pix, n_obs, spectra, qa, sec, nt);  /* a strict observation with data */
             break;
         }
-        for (int b = 0; b < 7; ++b)  /* band padding (the scalar path may have written a dropped value there) */
+        for (int b = 0; b < 7; ++b)  /* band padding: deterministic bytes */
             memset(bands + (size_t)b * bstride + tot, 0, 2 * (bstride - (size_t)tot));
         ret = sec_mode1(n_pix, n_obs, (int64_t)tot);
         break;

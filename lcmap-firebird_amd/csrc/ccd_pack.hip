@@ -151,6 +151,9 @@ __global__ __launch_bounds__(256) void ccd_decode_enc(const unsigned char *__res
     const unsigned char *q4 = sec + ENC_HDR + up16(4 * ((int64_t)n_pix + 1));
     const int64_t rowb = (n_obs + 1) / 2;
     const int16_t *bands = reinterpret_cast<const int16_t *>(q4 + up16((int64_t)n_pix * rowb)) + koff[p];
+    // the pixel's kept run (the host checked the table); a code row that claims more kept
+    // observations than the run holds reads no further than the run (its excess gets -9999)
+    const int kcount = (int)(koff[p + 1] - koff[p]);
     const unsigned char *qr = q4 + p * rowb;
     int carry = 0;
     // four 64-observation chunks per round: their code bytes load together, then their ranks,
@@ -182,7 +185,7 @@ __global__ __launch_bounds__(256) void ccd_decode_enc(const unsigned char *__res
         for (int u = 0; u < U; ++u) {
 #pragma unroll
             for (int b = 0; b < 7; ++b) v[u][b] = (int16_t)-9999;
-            if (keep[u]) {  // (loads under the lane's own mask: a dropped lane's rank may point past the column)
+            if (keep[u] && rank[u] < kcount) {  // (loads under the lane's own mask: a dropped lane's rank may point past the column)
 #pragma unroll
                 for (int b = 0; b < 7; ++b) v[u][b] = bands[b * bstride + rank[u]];
             }

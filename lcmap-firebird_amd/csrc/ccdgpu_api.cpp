@@ -224,6 +224,7 @@ struct ccdgpu_ctx {
     unsigned long long diag[CCD_NSTATS] = {};
     // a detection launched by ccdgpu_run_slot_begin and not yet finished by ccdgpu_run_slot_end
     bool pending = false;
+    int32_t pend_slot = -1;  // the upload slot that detection reads (not to be restaged until it ends)
     CcdDetectArgs pend_args{};
     ~ccdgpu_ctx() {
         for (auto *b : {&dates, &sdates, &offsets, &chip_obs_off, &chip_pix_off, &chip_data_off, &row_off, &seg_off1, &b64_off})
@@ -375,11 +376,19 @@ int ccdgpu_init_copy_cus(int device, int copy_cus, ccdgpu_ctx **out) {
     if (const char *e = std::getenv("CCDGPU_COPY_CUS")) copy_cus = std::max(0, std::atoi(e));
     std::vector<uint32_t> mask_det, mask_copy;
     if (copy_cus > 0 && copy_cus < c->n_cu) {
-        const int nw = (c->n_cu + 31) / 32, groups = 8, per = c->n_cu / groups, k = (copy_cus + groups - 1) / groups;
+        const int nw = (c->n_cu + 31) / 32, groups = 8, per = c->n_cu / groups;
+        // at least one CU of every group stays with the detection stream, and at least one is reserved
+        const int k = std::min((copy_cus + groups - 1) / groups, per - 1);
+        if (per < 2 || k < 1) {
+            const std::string msg = "copy_cus " + std::to_string(copy_cus) + " leaves no CU for detection or copies on " +
+                                    std::to_string(c->n_cu) + " CUs";
+            delete c;
+            return fail(CCDGPU_EINVAL, msg);
+        }
         mask_det.assign(nw, 0u);
         mask_copy.assign(nw, 0u);
         for (int cu = 0; cu < c->n_cu; ++cu) {
-            const bool reserved = per > k && (cu % per) >= per - k;
+            const bool reserved = (cu % per) >= per - k;
             (reserved ? mask_copy : mask_det)[cu / 32] |= 1u << (cu % 32);
         }
     }
@@ -614,6 +623,8 @@ int ccdgpu_stage_slot_chips(ccdgpu_ctx *c, int32_t slot, const ccdgpu_params *pa
     if (!c) return fail(CCDGPU_EINVAL, "NULL ctx");
     if (slot < 0 || slot >= CCDGPU_UPLOAD_SLOTS)
         return fail(CCDGPU_EINVAL, "slot must be in 0 .. " + std::to_string(CCDGPU_UPLOAD_SLOTS - 1));
+    if (c->pending && slot == c->pend_slot)
+        return fail(CCDGPU_EINVAL, "slot " + std::to_string(slot) + " is read by the detection begun with ccdgpu_run_slot_begin");
     if (!dates || !spectra || !qa) return fail(CCDGPU_EINVAL, "NULL input buffer");
     Shape sh;
     int rc = make_shape(n_chips, n_pix, n_obs, sh);
@@ -641,6 +652,8 @@ int ccdgpu_stage_slot_encoded(ccdgpu_ctx *c, int32_t slot, const ccdgpu_params *
     if (!c) return fail(CCDGPU_EINVAL, "NULL ctx");
     if (slot < 0 || slot >= CCDGPU_UPLOAD_SLOTS)
         return fail(CCDGPU_EINVAL, "slot must be in 0 .. " + std::to_string(CCDGPU_UPLOAD_SLOTS - 1));
+    if (c->pending && slot == c->pend_slot)
+        return fail(CCDGPU_EINVAL, "slot " + std::to_string(slot) + " is read by the detection begun with ccdgpu_run_slot_begin");
     if (!dates || !enc) return fail(CCDGPU_EINVAL, "NULL input buffer");
     Shape sh;
     int rc = make_shape(n_chips, n_pix, n_obs, sh);
@@ -660,6 +673,24 @@ int ccdgpu_stage_slot_encoded(ccdgpu_ctx *c, int32_t slot, const ccdgpu_params *
         if ((h[0] != 0 && h[0] != 1) || h[1] != n_pix[k] || h[2] != n_obs[k] || h64[1] != db ||
             (h[0] == 1 && (h[3] < 1 || h[3] > 16)))
             return fail(CCDGPU_EINVAL, "encoded batch: chip " + std::to_string(k) + " header does not match its shape");
+        // the section holds everything its mode's layout addresses (the decoder trusts it)
+        const int64_t np_ = n_pix[k], no_ = n_obs[k], plane = np_ * no_, sec = off[k + 1] - off[k];
+        auto up_ = [](int64_t x, int64_t a) { return (x + a - 1) / a * a; };
+        if (h[0] == 0) {
+            if (sec < 128 + up_(2 * plane, 16) + 14 * plane)
+                return fail(CCDGPU_EINVAL, "encoded batch: chip " + std::to_string(k) + " raw section is truncated");
+        } else {
+            const int64_t kept = h64[0], bstride = h64[2];
+            const int64_t bands_at = 128 + up_(4 * (np_ + 1), 16) + up_(np_ * ((no_ + 1) / 2), 16);
+            if (kept < 0 || kept > plane || bstride < kept || bstride % 8 != 0 || sec < bands_at + 14 * bstride)
+                return fail(CCDGPU_EINVAL, "encoded batch: chip " + std::to_string(k) + " band columns do not fit its section");
+            const uint32_t *koff = reinterpret_cast<const uint32_t *>(enc + off[k] + 128);
+            if (koff[0] != 0 || (int64_t)koff[np_] != kept)
+                return fail(CCDGPU_EINVAL, "encoded batch: chip " + std::to_string(k) + " kept-offset table does not end at kept");
+            for (int64_t q = 0; q < np_; ++q)
+                if (koff[q + 1] < koff[q] || (int64_t)(koff[q + 1] - koff[q]) > no_)
+                    return fail(CCDGPU_EINVAL, "encoded batch: chip " + std::to_string(k) + " kept-offset table is not a run per pixel");
+        }
         pb += n_pix[k];
         db += (int64_t)n_pix[k] * n_obs[k];
     }
@@ -721,6 +752,7 @@ int ccdgpu_run_slot_begin(ccdgpu_ctx *c, int32_t slot) {
     detect_args(c, c->pend_args);
     if ((rc = launch(c, c->pend_args))) return rc;
     c->pending = true;
+    c->pend_slot = slot;
     return 0;
 }
 
@@ -738,6 +770,7 @@ int ccdgpu_run_slot_end(ccdgpu_ctx *c, double *kernel_seconds) {
     if (!c->pending) return fail(CCDGPU_EINVAL, "no detection begun with ccdgpu_run_slot_begin");
     HIPCHK(hipSetDevice(c->device));
     c->pending = false;
+    c->pend_slot = -1;
     for (int attempt = 0; attempt < 4; ++attempt) {
         bool again = false;
         const int rc = finish(c, kernel_seconds, &again);

@@ -145,3 +145,35 @@ def test_word_outside_the_palette_sample_reencodes_the_same_bytes():
     if outs['0'][0] == 0:
         pytest.skip('no AVX-512 VBMI2 on this CPU: only the scalar encoder ran')
     assert outs['0'][1:] == outs['1'][1:]
+
+
+def test_scalar_encoder_dropped_last_observation_at_thread_boundaries():
+    """Scalar encoder (CCDGPU_ENCODE_SCALAR=1), 4 threads, the 'unread' drop: every pixel's last
+    observation is a dropped (cloud) one with data in its bands, and the kept total is a multiple
+    of 8 (band stride = kept total, no padding).  The scalar compaction once wrote each dropped
+    value one past the pixel's kept run -- over the next pixel's first kept value (the next
+    thread's, at a chunk boundary) or, after the last pixel, over the next band's first value."""
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); import ccdgpu; "
+            "n = 21; P = 64; rng = np.random.default_rng(11); d = np.arange(n, dtype=np.int64) * 16 + 730000; "
+            "q = np.full((P, n), 322, dtype=np.uint16); q[:, n - 1] = 322 | 32; q[:, 4] = 1; "
+            "s = rng.integers(0, 5000, size=(7, P, n)).astype(np.int16); s[:, :, 4] = -9999; "
+            "drop, strict = ccdgpu.unread_drop_bits(None); "
+            "e = ccdgpu.EncodedBatch.encode([(d, s, q)], threads=4, pinned=False, drop_bits=drop, strict_bits=strict); "
+            "sys.stdout.buffer.write(e.buf[:e.nbytes_encoded].tobytes())"
+            % os.path.join(ROOT, 'lcmap-firebird_amd'))
+    env = dict(os.environ, CCDGPU_ENCODE_SCALAR='1')
+    out = subprocess.run([sys.executable, '-c', code], env=env, capture_output=True, check=True).stdout
+    n, P = 21, 64
+    assert (P * (n - 2)) % 8 == 0
+    rng = np.random.default_rng(11)
+    q = np.full((P, n), 322, dtype=np.uint16)
+    q[:, n - 1] = 322 | 32
+    q[:, 4] = 1
+    s = rng.integers(0, 5000, size=(7, P, n)).astype(np.int16)
+    s[:, :, 4] = -9999
+    (ds, dq), = decode(np.frombuffer(out, dtype=np.uint8))
+    np.testing.assert_array_equal(dq, q)
+    keep = np.ones(n, dtype=bool)
+    keep[[4, n - 1]] = False
+    np.testing.assert_array_equal(ds[:, :, keep], s[:, :, keep])
+    assert (ds[:, :, ~keep] == -9999).all()

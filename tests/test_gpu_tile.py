@@ -69,3 +69,72 @@ def test_tile_runner_rows_match_oracle_and_batching():
     # and so do contexts without CUs reserved for the upload stream (ccdgpu_init_copy_cus)
     res4, _ = run(2, 3, copy_cus=0)
     assert [c['digest'] for c in res4['chips']] == [c['digest'] for c in res['chips']]
+
+
+# ---- full-size chips through the product defaults ---------------------------------------------
+FULL_CHIPS = 24
+
+
+def _full_cfg_id(p):
+    """(config, generator chip id) of tile position p: change-dense C5 chips mixed into C3 tile
+    chips, ids spread over the tile so both cadences (1421 / 2121 obs) occur"""
+    from ccdgpu import synth
+    return synth.config(5 if p % 3 == 2 else 3), 97 * p + 11
+
+
+class _FullSource(object):
+    """full 10^4-pixel chips generated on the GPU (one generator per fetch thread), pinned"""
+
+    def __init__(self):
+        import threading
+        self._local = threading.local()
+        self.gens = []
+
+    def __call__(self, positions):
+        import ccdgpu
+        from ccdgpu import synth
+        g = getattr(self._local, 'g', None)
+        if g is None:
+            g = self._local.g = synth.DeviceGenerator(0)
+            self.gens.append(g)
+        chips = []
+        for p in positions:
+            cfg, cid = _full_cfg_id(p)
+            chips.append(g.batch(cfg, [cid], n_pix=10000, pinned=False).chip(0))
+        return ccdgpu.ChipBatch.from_chips(chips, pinned=True)
+
+
+def _full_inputs(pos, pixels):
+    from ccdgpu import synth
+    cfg, cid = _full_cfg_id(pos)
+    parts = [synth.chip(cfg, cid, px, 1) for px in pixels]
+    d = parts[0][0]
+    return d, np.concatenate([s for _, s, _ in parts], axis=1), np.concatenate([q for _, _, q in parts], axis=0)
+
+
+def test_full_size_tile_with_product_defaults_matches_oracle_on_stratified_pixels():
+    """ccdc.runner.changedetection as the tile leg runs it -- 4 contexts per GPU, 8-chip launches,
+    8 CUs reserved per context for uploads, the 'unread' transport encoding, upload depth 2, split
+    run with staging during detection -- over 24 distinct full-size (10^4-pixel) chips of both
+    cadences with change-dense C5 chips mixed in (reference tile loop core.py:97-108 over
+    ccd.detect, pyccd.py:168); 100 stratified pixels per chip (one in every row) re-detected by
+    the C oracle: rows, days, curve QA, masks bit-exact, floats within 1e-6."""
+    import time
+    from ccdc import runner
+    import tile_sample
+    sink = tile_sample.PixelSampleSink(lambda pos: tile_sample.stratified(pos, 100))
+    src = _FullSource()
+    t = time.time()
+    res = runner.changedetection(tile(), src, device=0, number=FULL_CHIPS, sink=sink, tail_chips=4)
+    run_s = time.time() - t
+    for g in src.gens:
+        g.close()
+    assert [c['pos'] for c in res['chips']] == list(range(FULL_CHIPS))
+    assert {c['n_obs'] for c in res['chips']} == {1421, 2121}
+    assert all(c['n_pix'] == 10000 for c in res['chips'])
+    st = res['ranks'][0]
+    assert st['batches'] <= 6, st  # (8-chip launches, not the tail's quarter batches throughout)
+    out = tile_sample.check(sink, _full_inputs, threads=16)
+    print('full-size tile parity: %s, runner %.1f s' % (out, run_s))
+    assert out['pixels'] >= 100 * FULL_CHIPS - 5 and out['chips'] == FULL_CHIPS
+    assert out['int_mismatches'] == 0 and out['float_mismatches'] == 0, out

@@ -186,3 +186,76 @@ def test_tail_batches_shrink_near_the_end_of_the_queue():
     assert runner._pull_size(q, 8, 16) == 8
     q.next(30)
     assert runner._pull_size(q, 8, 16) == 2
+
+
+def test_pixel_sample_checker_passes_oracle_rows_and_flags_a_corrupted_one():
+    """tests/tile_sample.py (the sampled-pixel parity behind the GPU full-size tile test and the
+    bench's tile.parity_sample): rows from an oracle-backed run compare equal; a changed break day
+    and a flipped mask bit are reported as integer mismatches."""
+    from ccdc import runner
+    from ccdgpu import synth
+    from rows_util import OracleContext
+    import tile_sample
+    sink = tile_sample.PixelSampleSink(lambda pos: tile_sample.stratified(pos, 4, n_pix=N_PIX, width=N_PIX))
+    runner.changedetection(tile(), source, contexts=2, batch_chips=2, number=6, sink=sink,
+                           context_factory=lambda dev: OracleContext(dev, threads=2))
+
+    def inputs(pos, pixels):
+        d, s, q = synth.chip(synth.config(3), pos, 0, N_PIX)
+        return d, s[:, pixels], q[pixels]
+
+    out = tile_sample.check(sink, inputs, threads=4)
+    assert out['pixels'] == 24 and out['chips'] == 6
+    assert out['int_mismatches'] == 0 and out['float_mismatches'] == 0, out
+    cx, cy, n_obs, keep = sink.samples[3]
+    px = sorted(keep)[1]
+    rows, mask = keep[px]
+    rows['bday'][0] += 1
+    mask = mask.copy()
+    mask[0] ^= 1
+    keep[px] = (rows, mask)
+    px2 = sorted(keep)[2]
+    keep[px2] = (keep[px2][0], keep[px2][1] ^ np.uint32(4))
+    out = tile_sample.check(sink, inputs, threads=4)
+    assert out['int_mismatches'] == 2, out
+
+
+def _rank4(rank, world, port, q):
+    sys.path[:0] = [os.path.join(ROOT, 'tests'), os.path.join(ROOT, 'oracle'), os.path.join(ROOT, 'lcmap-firebird_amd')]
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from ccdc import runner
+    from rows_util import OracleContext
+    delay = 2.0 if rank == 3 else 0.0  # one slow rank
+    res = runner.changedetection(tile(), source, contexts=1, batch_chips=1, number=24,
+                                 context_factory=lambda dev: OracleContext(dev, threads=1, delay=delay))
+    q.put((rank, res))
+    dist.destroy_process_group()
+
+
+def test_one_tile_split_over_world4_with_a_slow_rank():
+    """The north-star mode (bench.py --tile-split; reference core.py:97-108): ONE tile's positions
+    shared by four ranks through the store queue, one rank slow -- every position is detected
+    exactly once, the slow rank takes fewer chips, and every rank's statistics carry its tail
+    (seconds from the first empty-queue pull to its end) for rank 0."""
+    import torch.multiprocessing as mp
+    world = 4
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank4, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(out[r] is None for r in (1, 2, 3))
+    res = out[0]
+    assert [c['pos'] for c in res['chips']] == list(range(24))
+    st = {s['rank']: s for s in res['ranks']}
+    assert sorted(st) == [0, 1, 2, 3]
+    assert sum(s['chips'] for s in st.values()) == 24
+    assert st[3]['chips'] < max(st[r]['chips'] for r in (0, 1, 2))
+    assert all('tail_seconds' in s and s['tail_seconds'] >= 0.0 for s in st.values())
