@@ -48,6 +48,9 @@ struct CcdDetectArgs {
     const int64_t *chip_data_off;  // [n_chips + 1]
     const int16_t *spectra;
     const uint16_t *qa;
+    // non-null: the batch's inputs are a transport-encoded batch (include/ccdgpu.h) read in place
+    // by the detection kernel (spectra / qa unused)
+    const unsigned char *enc;
     const int32_t *order;
     const int64_t *sdates;
     const double *basis;

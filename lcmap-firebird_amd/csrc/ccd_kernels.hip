@@ -83,6 +83,11 @@ struct __attribute__((aligned(16))) Lds {
             double tchol[5][5];    // Tmask: Cholesky factor of the unweighted normal matrix
             double tsys[2][5][6];  // paired Tmask: each band's weighted normal matrix | rhs
         };
+        struct {                   // px_setup of a transport-encoded pixel (read in place):
+            unsigned long long ekm[CCDGPU_MAX_OBS / 64];  // sent-band bits per 64 input observations
+            uint16_t ekp[CCDGPU_MAX_OBS / 64];            // sent observations before each chunk
+            uint16_t epal[16];                            // the chip's QA palette
+        };
     };
     // launch statistics of this wave (kept here, not in registers: they are only touched per fit
     // and at the end): [0] band fits, [1] CD sweeps, [2] counted FP64 flops.  Last member: the
@@ -3245,19 +3250,96 @@ __device__ __forceinline__ void standard_procedure(Px &P, int proc) {
 }
 
 // ------------------------------------------------------------------ qa.py filters + compaction
+// A pixel's inputs are read where they lie: the standard band-major layout (a plain upload, the
+// chipmunk decoder), a raw section of a transport-encoded batch (the same layout at the section's
+// own base pointers), or an encoded section (include/ccdgpu.h; ccd_encode.c) -- QA as 4-bit
+// palette codes, band values sent only for observations without a drop bit, compacted per pixel.
+// An encoded pixel is read in place, so the upload needs no decode pass (the standalone decoder
+// ccd_decode_enc in ccd_pack.hip is the same mapping): pass 1 walks the code row in input order
+// (class counts are order-free) and leaves, per 64 input observations, the bit mask of the
+// observations whose bands were sent and the count before them in LDS; pass 2 gathers in date
+// order, an observation's band values at its rank among the sent ones (-9999, the ARD fill value
+// the encoder dropped, for the others).
 // Returns the procedure, or -1 for an unsupported QA value.
 __device__ __forceinline__ int px_setup(Px &P, int chip, int pix) {
     const CcdDetectArgs &A = ARGS();
     const ccdgpu_params &p = A.p;
+    Lds *L = &LDS();
     const int l = lane();
     const int n = P.n;
-    const int64_t data_off = A.chip_data_off[chip];
     const int32_t *order = A.order + A.chip_obs_off[chip];
-    const uint16_t *qa = A.qa + data_off + (size_t)pix * n;
-    const size_t bstride = (size_t)(A.chip_pix_off[chip + 1] - A.chip_pix_off[chip]) * n;
-    const int16_t *sp = A.spectra + (size_t)NB * data_off + (size_t)pix * n;
+    const uint16_t *qa;
+    const int16_t *sp;
+    size_t bstride;
+    const unsigned char *codes = nullptr;  // encoded: the pixel's code row
+    int kcount = 0;                        // encoded: observations whose bands were sent
+    unsigned drop = 0u;
+    bool enc = false;
+    if (A.enc) {
+        const unsigned char *sec = A.enc + reinterpret_cast<const int64_t *>(A.enc)[1 + chip];
+        const int32_t *h = reinterpret_cast<const int32_t *>(sec);
+        const int64_t cpix = h[1];
+        const int64_t plane = cpix * n;
+        if (h[0] == 0) {
+            qa = reinterpret_cast<const uint16_t *>(sec + 128) + (size_t)pix * n;
+            sp = reinterpret_cast<const int16_t *>(sec + 128 + ((2 * plane + 15) & ~(int64_t)15)) + (size_t)pix * n;
+            bstride = (size_t)plane;
+        } else {
+            enc = true;
+            bstride = (size_t)reinterpret_cast<const int64_t *>(sec + 48)[2];
+            const uint32_t *koff = reinterpret_cast<const uint32_t *>(sec + 128);
+            const unsigned char *q4 = sec + 128 + ((4 * (cpix + 1) + 15) & ~(int64_t)15);
+            const int64_t rowb = (n + 1) / 2;
+            codes = q4 + (size_t)pix * rowb;
+            const uint32_t k0 = koff[pix];
+            kcount = (int)(koff[pix + 1] - k0);
+            sp = reinterpret_cast<const int16_t *>(q4 + ((cpix * rowb + 15) & ~(int64_t)15)) + k0;
+            qa = nullptr;
+            drop = *reinterpret_cast<const uint32_t *>(sec + 80);
+            if (l < 16) L->epal[l] = reinterpret_cast<const uint16_t *>(sec + 16)[l];
+            wsync();
+        }
+    } else {
+        const int64_t data_off = A.chip_data_off[chip];
+        qa = A.qa + data_off + (size_t)pix * n;
+        bstride = (size_t)(A.chip_pix_off[chip + 1] - A.chip_pix_off[chip]) * n;
+        sp = A.spectra + (size_t)NB * data_off + (size_t)pix * n;
+    }
     int c_clear = 0, c_water = 0, c_snow = 0, c_cloud = 0, c_fill = 0;
     bool bad = false;
+    if (enc) {
+        // input order: code bytes read contiguously (four chunks' loads together), palette in LDS
+        constexpr int U = 4;
+        int sent = 0;
+        for (int base0 = 0; base0 < n; base0 += U * W) {
+            unsigned cb[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = base0 + u * W + l;
+                cb[u] = i < n ? (unsigned)codes[i >> 1] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = base0 + u * W + l;
+                const bool in = i < n;
+                const unsigned q = L->epal[(cb[u] >> ((i & 1) * 4)) & 15u];
+                const int cls = in ? (p.qa_bitpacked ? qabitval(p, q) : (int)q) : -2;
+                c_clear += popc(bal(in && cls == p.qa_clear));
+                c_water += popc(bal(in && cls == p.qa_water));
+                c_snow += popc(bal(in && cls == p.qa_snow));
+                c_cloud += popc(bal(in && cls == p.qa_cloud));
+                c_fill += popc(bal(in && cls == p.qa_fill));
+                if (bal(in && cls < 0)) bad = true;
+                const unsigned long long km = bal(in && !(q & drop));
+                if (l == 0 && base0 + u * W < n) {
+                    L->ekm[(base0 >> 6) + u] = km;
+                    L->ekp[(base0 >> 6) + u] = (uint16_t)sent;
+                }
+                sent += popc(km);
+            }
+        }
+        wsync();
+    } else {
     // (four 64-observation chunks per round, their dependent order -> qa loads issued together;
     // the next round's order loads go out with this round's qa loads)
     constexpr int U = 4;
@@ -3288,6 +3370,7 @@ __device__ __forceinline__ int px_setup(Px &P, int chip, int pix) {
             c_fill += popc(bal(i < n && cls == p.qa_fill));
             if (bal(i < n && cls < 0)) bad = true;
         }
+    }
     }
     if (bad) return -1;
     const int total = n - c_fill;
@@ -3322,6 +3405,29 @@ __device__ __forceinline__ int px_setup(Px &P, int chip, int pix) {
         int16_t v2[U2][NB];
 #pragma unroll
         for (int u = 0; u < U2; ++u) o2[u] = on2[u];
+        if (enc) {
+            unsigned cb[U2];
+#pragma unroll
+            for (int u = 0; u < U2; ++u) cb[u] = base0 + u * W + l < n ? (unsigned)codes[o2[u] >> 1] : 0u;
+#pragma unroll
+            for (int u = 0; u < U2; ++u) {
+                const int i = base0 + u * W + l;
+                const bool valid = i < n;
+                const int o = o2[u];
+                const unsigned q = L->epal[(cb[u] >> ((o & 1) * 4)) & 15u];
+                q2[u] = valid ? q : 0u;
+                const int w = o >> 6;
+                const int r = (int)L->ekp[w] + popc(L->ekm[w] & ((1ull << (o & 63)) - 1ull));
+                const bool have = valid && !(q & drop) && r < kcount;
+#pragma unroll
+                for (int b = 0; b < NB; ++b) v2[u][b] = valid ? (int16_t)-9999 : (int16_t)0;
+                if (have) {
+#pragma unroll
+                    for (int b = 0; b < NB; ++b) v2[u][b] = sp[(size_t)b * bstride + r];
+                }
+                d2[u] = valid ? (int)P.sd[i] : 0;
+            }
+        } else {
 #pragma unroll
         for (int u = 0; u < U2; ++u) {
             const int i = base0 + u * W + l;
@@ -3330,6 +3436,7 @@ __device__ __forceinline__ int px_setup(Px &P, int chip, int pix) {
 #pragma unroll
             for (int b = 0; b < NB; ++b) v2[u][b] = valid ? sp[(size_t)b * bstride + o2[u]] : (int16_t)0;
             d2[u] = valid ? (int)P.sd[i] : 0;
+        }
         }
 #pragma unroll
         for (int u = 0; u < U2; ++u) {

@@ -176,6 +176,9 @@ struct ccdgpu_ctx {
     const int64_t *in_dates = nullptr;
     const int16_t *in_spectra = nullptr;
     const uint16_t *in_qa = nullptr;
+    const unsigned char *in_enc = nullptr;  // a transport-encoded batch the kernel reads in place
+    // decode encoded uploads into the standard layout first (CCDGPU_DECODE=1: the round-3 path, A/B)
+    bool decode_enc = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // the host waits for a detection through this event: blocking (the waiting thread sleeps on
     // the completion interrupt instead of polling), so the tile driver's waiting workers leave the
@@ -217,6 +220,7 @@ struct ccdgpu_ctx {
     Shape slot_shape[CCDGPU_UPLOAD_SLOTS];
     ccdgpu_params slot_params[CCDGPU_UPLOAD_SLOTS];
     bool slot_ready[CCDGPU_UPLOAD_SLOTS] = {};
+    bool slot_encoded[CCDGPU_UPLOAD_SLOTS] = {};  // the slot holds an encoded batch read in place
     DevBuf<unsigned char> b64;  // chipmunk payload text of the last ccdgpu_stage_chipmunk
     DevBuf<int64_t> b64_off;
     std::vector<int64_t> h_offsets;
@@ -427,6 +431,7 @@ int ccdgpu_init_copy_cus(int device, int copy_cus, ccdgpu_ctx **out) {
     }
     if (const char *v = std::getenv("CCDGPU_SLOTS_PER_CU")) c->slots_per_cu = std::max(1, std::atoi(v));
     if (const char *v = std::getenv("CCDGPU_POISON")) c->poison = std::atoi(v) != 0;
+    if (const char *v = std::getenv("CCDGPU_DECODE")) c->decode_enc = std::atoi(v) != 0;
     *out = c;
     return 0;
 }
@@ -519,6 +524,7 @@ static int stage_alloc(ccdgpu_ctx *c, const ccdgpu_params *params, const Shape &
     c->in_dates = c->dates.p;
     c->in_spectra = c->spectra.p;
     c->in_qa = c->qa.p;
+    c->in_enc = nullptr;
     return 0;
 }
 
@@ -643,6 +649,7 @@ int ccdgpu_stage_slot_chips(ccdgpu_ctx *c, int32_t slot, const ccdgpu_params *pa
     c->slot_shape[slot] = sh;
     c->slot_params[slot] = *params;  // each slot keeps its own parameters
     c->slot_ready[slot] = true;
+    c->slot_encoded[slot] = false;
     return 0;
 }
 
@@ -697,19 +704,23 @@ int ccdgpu_stage_slot_encoded(ccdgpu_ctx *c, int32_t slot, const ccdgpu_params *
     if (pixo[n_chips] != pb) return fail(CCDGPU_EINVAL, "encoded batch: pixel total does not match");
     HIPCHK(hipSetDevice(c->device));
     const size_t tobs = (size_t)sh.total_obs(), tdata = (size_t)sh.total_data();
-    if ((rc = c->slot_dates[slot].ensure(tobs)) || (rc = c->slot_spectra[slot].ensure(7 * tdata)) ||
-        (rc = c->slot_qa[slot].ensure(tdata)) || (rc = c->slot_enc[slot].ensure((size_t)off[n_chips])))
+    if ((rc = c->slot_dates[slot].ensure(tobs)) || (rc = c->slot_enc[slot].ensure((size_t)off[n_chips])))
         return rc;
-    // upload on the copy stream, then decode there into the slot's standard buffers; run_slot
-    // waits for both through the slot's event
+    if (c->decode_enc && ((rc = c->slot_spectra[slot].ensure(7 * tdata)) || (rc = c->slot_qa[slot].ensure(tdata))))
+        return rc;
+    // upload on the copy stream; the detection kernel reads the encoded batch in place (no decode
+    // pass: px_setup in ccd_kernels.hip), or -- CCDGPU_DECODE=1 -- it is decoded there into the
+    // slot's standard buffers first.  run_slot waits for the copy stream through the slot's event.
     HIPCHK(hipMemcpyAsync(c->slot_dates[slot].p, dates, sizeof(int64_t) * tobs, hipMemcpyHostToDevice, c->copy_stream));
     HIPCHK(hipMemcpyAsync(c->slot_enc[slot].p, enc, (size_t)off[n_chips], hipMemcpyHostToDevice, c->copy_stream));
-    if (ccdk_decode_enc(c->slot_enc[slot].p, pb, c->slot_spectra[slot].p, c->slot_qa[slot].p, c->copy_stream))
+    if (c->decode_enc &&
+        ccdk_decode_enc(c->slot_enc[slot].p, pb, c->slot_spectra[slot].p, c->slot_qa[slot].p, c->copy_stream))
         return fail(CCDGPU_EHIP, "ccd_decode_enc launch failed");
     HIPCHK(hipEventRecord(c->uploaded[slot], c->copy_stream));
     c->slot_shape[slot] = sh;
     c->slot_params[slot] = *params;
     c->slot_ready[slot] = true;
+    c->slot_encoded[slot] = !c->decode_enc;
     return 0;
 }
 
@@ -728,8 +739,9 @@ static int slot_inputs(ccdgpu_ctx *c, int32_t slot) {
     if (rc) return rc;
     HIPCHK(hipStreamWaitEvent(c->aux, c->uploaded[slot], 0));
     c->in_dates = c->slot_dates[slot].p;
-    c->in_spectra = c->slot_spectra[slot].p;
-    c->in_qa = c->slot_qa[slot].p;
+    c->in_enc = c->slot_encoded[slot] ? c->slot_enc[slot].p : nullptr;
+    c->in_spectra = c->slot_encoded[slot] ? nullptr : c->slot_spectra[slot].p;
+    c->in_qa = c->slot_encoded[slot] ? nullptr : c->slot_qa[slot].p;
     c->staged = true;
     c->ran = false;
     c->slot_ready[slot] = false;
@@ -784,9 +796,21 @@ int ccdgpu_staged_inputs(ccdgpu_ctx *c, int16_t *spectra, uint16_t *qa) {
     if (!c || !c->staged) return fail(CCDGPU_EINVAL, "nothing staged");
     HIPCHK(hipSetDevice(c->device));
     const size_t tdata = (size_t)c->shape.total_data();
+    const int16_t *ins = c->in_spectra;
+    const uint16_t *inq = c->in_qa;
+    if (c->in_enc) {
+        // an encoded batch read in place by the detection: decoded here (the standalone decoder,
+        // the same mapping as px_setup's) into the context's standard buffers
+        int rc;
+        if ((rc = c->spectra.ensure(7 * tdata)) || (rc = c->qa.ensure(tdata))) return rc;
+        if (ccdk_decode_enc(c->in_enc, c->shape.total_pix(), c->spectra.p, c->qa.p, c->stream))
+            return fail(CCDGPU_EHIP, "ccd_decode_enc launch failed");
+        ins = c->spectra.p;
+        inq = c->qa.p;
+    }
     if (spectra)
-        HIPCHK(hipMemcpyAsync(spectra, c->in_spectra, sizeof(int16_t) * 7 * tdata, hipMemcpyDeviceToHost, c->stream));
-    if (qa) HIPCHK(hipMemcpyAsync(qa, c->in_qa, sizeof(uint16_t) * tdata, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(spectra, ins, sizeof(int16_t) * 7 * tdata, hipMemcpyDeviceToHost, c->stream));
+    if (qa) HIPCHK(hipMemcpyAsync(qa, inq, sizeof(uint16_t) * tdata, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
 }
@@ -809,6 +833,7 @@ static void detect_args(ccdgpu_ctx *c, CcdDetectArgs &a) {
     a.chip_data_off = c->chip_data_off.p;
     a.spectra = c->in_spectra;
     a.qa = c->in_qa;
+    a.enc = c->in_enc;
     a.order = c->order.p;
     a.sdates = c->sdates.p;
     a.basis = c->basis.p;

@@ -36,7 +36,7 @@ for r in range(a.rounds):
         os.environ['CCDGPU_KERNEL'] = variant or 'w3'
         ccdgpu._lib = None
         ccdgpu.LIB_PATH = path if os.path.isabs(path) else os.path.join(ROOT, 'lcmap-firebird_amd', path)
-        ns = argparse.Namespace(chips=a.chips, contexts=a.contexts, warmup=a.warmup, steps=a.steps, config=a.config)
+        ns = argparse.Namespace(chips=a.chips, contexts=a.contexts, warmup=a.warmup, steps=a.steps, config=a.config, roofline_launches=1)
         out = bench.resident_leg(ns, cfg, 0, 1, 0, None, batch=batch)
         rate = out['value']
         res.setdefault(spec, []).append({'value': rate, 'frac': out['roofline']['frac'],
