@@ -154,6 +154,21 @@ int make_shape(int32_t n_chips, const int32_t *n_pix, const int32_t *n_obs, Shap
     return 0;
 }
 
+// One upload stream per device shared by every context (unless CCDGPU_SHARED_UPLOADS=0):
+// the host-to-device copies of all contexts then run one after another in the order they were
+// staged -- the order their detections need them -- instead of side by side on separate DMA
+// queues, where every upload in flight shares the link and each finishes late.  Created on first
+// use, kept for the process's lifetime.
+std::mutex g_up_mu;
+hipStream_t g_up_stream[64] = {};
+hipStream_t shared_upload_stream(int device) {
+    if (device < 0 || device >= 64) return nullptr;
+    std::lock_guard<std::mutex> g(g_up_mu);
+    if (!g_up_stream[device] && hipStreamCreateWithFlags(&g_up_stream[device], hipStreamNonBlocking) != hipSuccess)
+        g_up_stream[device] = nullptr;
+    return g_up_stream[device];
+}
+
 }  // namespace
 
 struct ccdgpu_ctx {
@@ -165,6 +180,7 @@ struct ccdgpu_ctx {
     int arg_slot = -1;  // this context's launch-argument slot in constant memory
     hipStream_t stream = nullptr;
     hipStream_t copy_stream = nullptr;  // uploads of ccdgpu_stage_slot (overlap a running detection)
+    hipStream_t up_stream = nullptr;    // where the slot uploads go: copy_stream, or the device's shared one
     // every other kernel and copy of a launch (prep, CSR scan and scatter, row packing, small
     // copies): the detection stream itself, or -- with CUs reserved (ccdgpu_init_copy_cus) -- a
     // stream on the reserved CUs, so these short kernels never wait for wave slots behind
@@ -410,6 +426,17 @@ int ccdgpu_init_copy_cus(int device, int copy_cus, ccdgpu_ctx **out) {
         return fail(CCDGPU_EHIP, "hipStreamCreate failed");
     }
     for (auto &e : c->uploaded) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    // uploads in staging order on the device's shared stream (default; CCDGPU_SHARED_UPLOADS=0:
+    // each context's own copy stream).  Tile leg A/B: 2.50 / 2.62M vs 2.42 / 2.50M px/s
+    // (profiles/r04/tile_knobs.json).
+    c->up_stream = c->copy_stream;
+    {
+        const char *v = std::getenv("CCDGPU_SHARED_UPLOADS");
+        if (!v || std::atoi(v) != 0) {
+            hipStream_t sh = shared_upload_stream(device);
+            if (sh) c->up_stream = sh;
+        }
+    }
     c->aux = c->stream;
     if (masked) {
         if (hipExtStreamCreateWithCUMask(&c->aux, (uint32_t)mask_copy.size(), mask_copy.data()) != hipSuccess) {
@@ -441,6 +468,7 @@ int ccdgpu_destroy(ccdgpu_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipStreamSynchronize(ctx->copy_stream);
+    if (ctx->up_stream && ctx->up_stream != ctx->copy_stream) (void)hipStreamSynchronize(ctx->up_stream);
     if (ctx->aux) (void)hipStreamSynchronize(ctx->aux);
     delete ctx;
     return 0;
@@ -642,10 +670,10 @@ int ccdgpu_stage_slot_chips(ccdgpu_ctx *c, int32_t slot, const ccdgpu_params *pa
         return rc;
     // the slot's previous batch was detected by a ccdgpu_run_slot that has returned, so the
     // uploads may overwrite it; they run on the copy stream, concurrent with any detection
-    HIPCHK(hipMemcpyAsync(c->slot_dates[slot].p, dates, sizeof(int64_t) * tobs, hipMemcpyHostToDevice, c->copy_stream));
-    HIPCHK(hipMemcpyAsync(c->slot_spectra[slot].p, spectra, sizeof(int16_t) * 7 * tdata, hipMemcpyHostToDevice, c->copy_stream));
-    HIPCHK(hipMemcpyAsync(c->slot_qa[slot].p, qa, sizeof(uint16_t) * tdata, hipMemcpyHostToDevice, c->copy_stream));
-    HIPCHK(hipEventRecord(c->uploaded[slot], c->copy_stream));
+    HIPCHK(hipMemcpyAsync(c->slot_dates[slot].p, dates, sizeof(int64_t) * tobs, hipMemcpyHostToDevice, c->up_stream));
+    HIPCHK(hipMemcpyAsync(c->slot_spectra[slot].p, spectra, sizeof(int16_t) * 7 * tdata, hipMemcpyHostToDevice, c->up_stream));
+    HIPCHK(hipMemcpyAsync(c->slot_qa[slot].p, qa, sizeof(uint16_t) * tdata, hipMemcpyHostToDevice, c->up_stream));
+    HIPCHK(hipEventRecord(c->uploaded[slot], c->up_stream));
     c->slot_shape[slot] = sh;
     c->slot_params[slot] = *params;  // each slot keeps its own parameters
     c->slot_ready[slot] = true;
@@ -711,12 +739,15 @@ int ccdgpu_stage_slot_encoded(ccdgpu_ctx *c, int32_t slot, const ccdgpu_params *
     // upload on the copy stream; the detection kernel reads the encoded batch in place (no decode
     // pass: px_setup in ccd_kernels.hip), or -- CCDGPU_DECODE=1 -- it is decoded there into the
     // slot's standard buffers first.  run_slot waits for the copy stream through the slot's event.
-    HIPCHK(hipMemcpyAsync(c->slot_dates[slot].p, dates, sizeof(int64_t) * tobs, hipMemcpyHostToDevice, c->copy_stream));
-    HIPCHK(hipMemcpyAsync(c->slot_enc[slot].p, enc, (size_t)off[n_chips], hipMemcpyHostToDevice, c->copy_stream));
-    if (c->decode_enc &&
-        ccdk_decode_enc(c->slot_enc[slot].p, pb, c->slot_spectra[slot].p, c->slot_qa[slot].p, c->copy_stream))
-        return fail(CCDGPU_EHIP, "ccd_decode_enc launch failed");
-    HIPCHK(hipEventRecord(c->uploaded[slot], c->copy_stream));
+    HIPCHK(hipMemcpyAsync(c->slot_dates[slot].p, dates, sizeof(int64_t) * tobs, hipMemcpyHostToDevice, c->up_stream));
+    HIPCHK(hipMemcpyAsync(c->slot_enc[slot].p, enc, (size_t)off[n_chips], hipMemcpyHostToDevice, c->up_stream));
+    HIPCHK(hipEventRecord(c->uploaded[slot], c->up_stream));
+    if (c->decode_enc) {
+        if (c->up_stream != c->copy_stream) HIPCHK(hipStreamWaitEvent(c->copy_stream, c->uploaded[slot], 0));
+        if (ccdk_decode_enc(c->slot_enc[slot].p, pb, c->slot_spectra[slot].p, c->slot_qa[slot].p, c->copy_stream))
+            return fail(CCDGPU_EHIP, "ccd_decode_enc launch failed");
+        HIPCHK(hipEventRecord(c->uploaded[slot], c->copy_stream));
+    }
     c->slot_shape[slot] = sh;
     c->slot_params[slot] = *params;
     c->slot_ready[slot] = true;

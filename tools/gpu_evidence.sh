@@ -14,12 +14,5 @@ timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smo
 tail -1 $O/smoke.log
 timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo "bench rc=$?"; tail -5 $O/bench.err; exit 1; }
 python3 -c "import json; d=json.load(open('$O/bench.json')); r=d['roofline']; print('bench', round(d['value']), 'resident', round(d['value_resident']), 'frac', round(r['frac'],4), 'launch_ms', round(r['kernel_ms_per_launch'],2), 'tile_s', round(d['tile']['seconds'],2), 'parity', d['tile'].get('parity_sample'), 'lossless', d.get('tile_lossless', {}).get('value'))"
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/stats -o run -- python3 $R/bench.py --no-tile --no-packer --no-cpu-baseline --contexts 1 --steps 6 --warmup 1 --roofline-launches 3 > $O/stats_bench.json 2> $O/stats_bench.err || { echo "stats rc=$?"; tail -5 $O/stats_bench.err; exit 1; }
-cd $R
-python3 tools/rocpd_stats.py $O/stats/run_results.db $O/kernel_stats.csv && head -4 $O/kernel_stats.csv
-if [ "${PMC:-0}" = 1 ]; then
-  bash tools/gpu_pmc.sh ${TAG}_pmc || { echo "pmc failed"; cat gpurun_out/${TAG}_pmc_rc.txt; exit 1; }
-  echo pmc ok
-fi
+PMC=${PMC:-0} bash tools/gpu_evidence_stats.sh $TAG || exit 1
 echo done

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Timeline of a traced tile run (rocprofv3 --kernel-trace --memory-copy-trace, rocpd database):
 over the timed window (the last `seconds` of the trace, from bench.py's tile JSON) the fraction
-of wall time covered by at least one detection kernel, by at least one host-to-device copy, by
+of wall time covered by at least one detection kernel, the time fractions with 0, 1, 2, ...
+detection launches in flight, by at least one host-to-device copy, by
 both, and by neither; the H2D bytes and rate; the detection kernels' summed durations; and the
 upload decode kernel's durations (median, max).
 
@@ -65,6 +66,15 @@ def main():
     dec = [e - s for n, s, e in c.execute('select name, start, end from kernels') if 'decode_enc' in n and s >= lo]
     both = intersect(d, h)
     wall = hi - lo
+    # how many detection launches are in flight at once (each is one context's batch): the time
+    # fraction with 0, 1, 2, ... of them -- with one alone the GPU is draining its tail
+    ev = sorted([(max(a, lo), 1) for a, b in det if b > lo and a < hi] + [(min(b, hi), -1) for a, b in det if b > lo and a < hi])
+    conc, cur, last = {}, 0, lo
+    for t, dlt in ev:
+        conc[cur] = conc.get(cur, 0) + (t - last)
+        cur += dlt
+        last = t
+    conc[cur] = conc.get(cur, 0) + (hi - last)
     out = {'window_s': wall / 1e9, 'detect_covered': length(d) / wall, 'h2d_covered': length(h) / wall,
            'both': length(both) / wall, 'neither': 1 - (length(d) + length(h) - length(both)) / wall,
            'h2d_bytes': nbytes, 'h2d_gbs_over_window': nbytes / wall, 'h2d_gbs_while_copying': nbytes / max(1, length(h)),
@@ -72,6 +82,8 @@ def main():
            'detect_kernel_seconds_summed': sum(b - a for a, b in det if a >= lo) / 1e9,
            'decode_dispatches': len(dec), 'decode_ms_median': (sorted(dec)[len(dec) // 2] / 1e6) if dec else None,
            'decode_ms_max': (max(dec) / 1e6) if dec else None,
+           'detections_in_flight_time_fraction': {str(k): round(v / wall, 4) for k, v in sorted(conc.items())},
+           'detect_ms_median': sorted(b - a for a, b in det if a >= lo)[len([1 for a, b in det if a >= lo]) // 2] / 1e6,
            'copy_kinds': sorted({str(r[ci['name']]) for r in rows}) if 'name' in ci else cols}
     print(json.dumps(out, indent=1))
 
