@@ -605,6 +605,7 @@ def tile_leg(args, cfg, rank, world, device, dist, split=False):
             'generate_seconds_rank0': round(gen_s, 3),
             'pinned_pool_batches': src.allocated,
             'worker_seconds_rank0': {k: round(v, 3) for k, v in ranks[0].items() if k.endswith('_seconds')},
+            'runner_trace_rank0': ranks[0].get('trace'),  # (CCDC_RUNNER_TRACE=1 only)
             'note': 'ccdc.runner tile driver over distinct chip inputs (pool mode: %d GPU-generated chips generated before '
                     'the timed run, each tile position a copy of one of its cadence with the acquisition dates moved by a '
                     'position-dependent multiple of 16 days; generate mode: every chip generated on the GPU into pinned '

@@ -227,6 +227,19 @@ int ccdgpu_run_slot(ccdgpu_ctx *ctx, int32_t slot, double *kernel_seconds);
 int ccdgpu_run_slot_begin(ccdgpu_ctx *ctx, int32_t slot);
 int ccdgpu_run_query(ccdgpu_ctx *ctx);
 int ccdgpu_run_slot_end(ccdgpu_ctx *ctx, double *kernel_seconds);
+/* The split run with the batch's rows in the same device chain (the tile driver's path; rows as
+ * ccdgpu_fetch_batch_rows_into gives them, chip c at (cx[c], cy[c])): _begin_rows enqueues the
+ * detection and behind it the CSR, the row packing and the copies of the row offsets
+ * [total_pixels + 1], the rows (up to rows_cap) and the mask words [total_pixels][mask_words]
+ * into the caller's buffers (pinned: ccdgpu_host_alloc), then returns; _end_rows waits once for
+ * the whole chain and returns what ccdgpu_run_slot_end returns, with the row count in *n_rows.
+ * More rows than rows_cap: CCDGPU_EOVERFLOW with *n_rows set -- the run is complete and
+ * ccdgpu_fetch_batch_rows_into fetches its rows into larger buffers.  The buffers must stay
+ * alive and untouched until _end_rows returns; ccdgpu_run_query works as for _begin. */
+int ccdgpu_run_slot_begin_rows(ccdgpu_ctx *ctx, int32_t slot, const int32_t *cx, const int32_t *cy, int32_t width,
+                               int64_t *row_offsets, int64_t offsets_cap, ccdgpu_row *rows, int64_t rows_cap,
+                               uint32_t *mask_bits, int64_t mask_cap);
+int ccdgpu_run_slot_end_rows(ccdgpu_ctx *ctx, double *kernel_seconds, int64_t *n_rows);
 
 /* Transport-encoded uploads (no reference counterpart -- the tile path's PCIe link is its bound,
  * DESIGN.md §5).  ccdgpu_encode_chips packs chips given as per-chip pointers (spectra
@@ -255,6 +268,12 @@ int64_t ccdgpu_encode_chips(int32_t n_chips, const int32_t *n_pix, const int32_t
                             const uint16_t *const *qa, uint8_t *out, int64_t out_cap, int32_t threads,
                             uint16_t drop_bits, uint16_t strict_bits);
 int32_t ccdgpu_encode_vector_path(void);
+/* The checks ccdgpu_stage_slot_encoded makes before an encoded batch is uploaded (no device
+ * needed): the chip table, every section's header against the chip's shape, every section long
+ * enough for its mode's layout, and each encoded section's kept-offset table a run per pixel
+ * ending at its kept count.  0, or CCDGPU_EINVAL with the reason in ccdgpu_last_error(). */
+int ccdgpu_encoded_check(int32_t n_chips, const int32_t *n_pix, const int32_t *n_obs, const uint8_t *enc,
+                         int64_t enc_bytes);
 int ccdgpu_stage_slot_encoded(ccdgpu_ctx *ctx, int32_t slot, const ccdgpu_params *params, int32_t n_chips,
                               const int32_t *n_pix, const int32_t *n_obs, const int64_t *dates, const uint8_t *enc,
                               int64_t enc_bytes);

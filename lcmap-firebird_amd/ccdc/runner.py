@@ -321,7 +321,11 @@ def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, er
     its rows are fetched (with one batch ahead the link idles whenever both of a GPU's contexts
     are past their upload).  The ARD of the next batches is fetched by the worker's own fetch
     thread (``_fetcher``) meanwhile.  Near the end of the queue the batches shrink (``_pull_size``)."""
+    import os
     import queue as queue_mod
+    # CCDC_RUNNER_TRACE=1: per-batch host timestamps (perf_counter) of this worker into
+    # stats['trace'] -- staged / launched / detection done / rows fetched (diagnostics)
+    trace = [] if os.environ.get('CCDC_RUNNER_TRACE') else None
     ready = queue_mod.Queue()
     stop = threading.Event()
     permits = threading.Semaphore(depth + 1)  # one per upload slot
@@ -337,6 +341,9 @@ def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, er
         if hasattr(ctx, 'fetch_batch_rows_into'):
             import ccdgpu
             into = ccdgpu.RowsBuffers()
+        # the rows come back in the detection's own device chain (one wait per batch instead of
+        # a wait for the detection and then the CSR, row packing and copies with their own waits)
+        chain = into is not None and hasattr(ctx, 'run_slot_begin_rows') and not os.environ.get('CCDC_NO_ROW_CHAIN')
         exhausted = False
         while True:
             while free and not exhausted:
@@ -355,15 +362,23 @@ def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, er
                 slot = free.pop(0)
                 ctx.stage_slot_chips(slot, batch, params)
                 staged.append((slot, pos, batch))
+                if trace is not None:
+                    trace.append(('stage', pos[0], t1))
                 with stats['lock']:
                     stats['stage_seconds'] += clock() - t1
             if not staged:
                 break
             s, ppos, pbatch = staged.pop(0)
+            cx = np.array([xys[p][0] for p in ppos], dtype=np.int32)
+            cy = np.array([xys[p][1] for p in ppos], dtype=np.int32)
             t2 = clock()
             t_in = 0.0  # staging done while the detection ran
+            got = None
             if split:
-                ctx.run_slot_begin(s)
+                if chain:
+                    ctx.run_slot_begin_rows(s, cx, cy, into, width)
+                else:
+                    ctx.run_slot_begin(s)
                 # while it runs, upload what the fetch thread finishes into the free slots (a
                 # batch otherwise waits for this detection and its row fetch to end)
                 while free and not exhausted and not ctx.run_done():
@@ -381,17 +396,24 @@ def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, er
                     slot = free.pop(0)
                     ctx.stage_slot_chips(slot, batch, params)
                     staged.append((slot, pos, batch))
+                    if trace is not None:
+                        trace.append(('stage', pos[0], t1))
                     t_in += clock() - t1
-                ctx.run_slot_end()
+                t_end = clock()
+                if chain:
+                    got = ctx.run_slot_end_rows()
+                else:
+                    ctx.run_slot_end()
             else:
+                t_end = clock()
                 ctx.run_slot(s)
             if getattr(ctx, 'qa_error', False):
                 import ccdgpu
                 raise ccdgpu.QAValueError('unsupported bit-packed QA value in chips at tile positions %s' % (ppos,))
             t3 = clock()
-            cx = np.array([xys[p][0] for p in ppos], dtype=np.int32)
-            cy = np.array([xys[p][1] for p in ppos], dtype=np.int32)
-            if into is not None:  # views of the landing buffers: valid until the next batch's fetch
+            if got is not None:  # views of the landing buffers: valid until the next batch
+                off, rows, mask = got
+            elif into is not None:  # views of the landing buffers: valid until the next batch's fetch
                 off, rows, mask = ctx.fetch_batch_rows_into(cx, cy, into, width)
             else:
                 off, rows, mask = ctx.fetch_batch_rows(cx, cy, width)
@@ -407,6 +429,9 @@ def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, er
             if release is not None:
                 release(pbatch)  # its upload is done and its rows are out: the source may reuse it
             t5 = clock()
+            if trace is not None:
+                # launch, (begin of) the wait for the detection, detection finished, rows fetched, sunk
+                trace.append(('run', ppos[0], t2, t_end, t3, t4, t5))
             with stats['lock']:
                 stats['batches'] += 1
                 stats['chips'] += len(ppos)
@@ -419,6 +444,10 @@ def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, er
     except BaseException as e:  # reported by detect_tile after the other workers drain
         errors.append(e)
     finally:
+        if trace is not None:
+            with stats['lock']:
+                stats.setdefault('trace', []).append([(x[0], x[1]) + tuple(round(v - stats['t0'], 5) for v in x[2:])
+                                                      for x in trace])
         stop.set()
         while ft.is_alive():  # unblock a fetcher waiting to put (its batch is dropped)
             try:

@@ -49,6 +49,12 @@ def _declare(L):
         L.ccdgpu_run_query.restype = c.c_int
         L.ccdgpu_run_slot_end.argtypes = [c.c_void_p, c.POINTER(c.c_double)]
         L.ccdgpu_run_slot_end.restype = c.c_int
+    if hasattr(L, 'ccdgpu_run_slot_begin_rows'):
+        L.ccdgpu_run_slot_begin_rows.argtypes = [c.c_void_p, c.c_int32, c.c_void_p, c.c_void_p, c.c_int32, c.c_void_p,
+                                                 c.c_int64, c.c_void_p, c.c_int64, c.c_void_p, c.c_int64]
+        L.ccdgpu_run_slot_begin_rows.restype = c.c_int
+        L.ccdgpu_run_slot_end_rows.argtypes = [c.c_void_p, c.POINTER(c.c_double), c.POINTER(c.c_int64)]
+        L.ccdgpu_run_slot_end_rows.restype = c.c_int
     if hasattr(L, 'ccdgpu_init_copy_cus'):
         L.ccdgpu_init_copy_cus.argtypes = [c.c_int, c.c_int, c.POINTER(c.c_void_p)]
         L.ccdgpu_init_copy_cus.restype = c.c_int
@@ -64,6 +70,9 @@ def _declare(L):
         L.ccdgpu_stage_slot_encoded.argtypes = [c.c_void_p, c.c_int32, c.c_void_p, c.c_int32, c.c_void_p, c.c_void_p,
                                                 c.c_void_p, c.c_void_p, c.c_int64]
         L.ccdgpu_stage_slot_encoded.restype = c.c_int
+    if hasattr(L, 'ccdgpu_encoded_check'):
+        L.ccdgpu_encoded_check.argtypes = [c.c_int32, c.c_void_p, c.c_void_p, c.c_void_p, c.c_int64]
+        L.ccdgpu_encoded_check.restype = c.c_int
     if hasattr(L, 'ccdgpu_device_numa_node'):  # (absent from libraries built before it: A/B runs)
         L.ccdgpu_device_numa_node.argtypes = [c.c_int, c.POINTER(c.c_int)]
         L.ccdgpu_device_numa_node.restype = c.c_int
@@ -111,7 +120,8 @@ EXPORTS = ('ccdgpu_version', 'ccdgpu_last_error', 'ccdgpu_params_default', 'ccdg
            'ccdgpu_last_stats', 'ccdgpu_diag_counters', 'ccdgpu_stage_chips', 'ccdgpu_stage_slot_chips',
            'ccdgpu_fetch_batch_rows', 'ccdgpu_device_numa_node', 'ccdgpu_encoded_bound', 'ccdgpu_encode_chips',
            'ccdgpu_encode_vector_path', 'ccdgpu_stage_slot_encoded', 'ccdgpu_init_copy_cus',
-           'ccdgpu_run_slot_begin', 'ccdgpu_run_query', 'ccdgpu_run_slot_end', 'ccdgpu_fetch_batch_rows_into')
+           'ccdgpu_run_slot_begin', 'ccdgpu_run_query', 'ccdgpu_run_slot_end', 'ccdgpu_fetch_batch_rows_into',
+           'ccdgpu_run_slot_begin_rows', 'ccdgpu_run_slot_end_rows', 'ccdgpu_encoded_check')
 
 
 def lib():
@@ -318,6 +328,12 @@ class EncodedBatch(ChipBatch):
         b = cls([c[2].shape[0] for c in chips], [c[0].shape[0] for c in chips], storage=storage, pinned=pinned)
         b.fill(chips, threads, drop_bits, strict_bits)
         return b
+
+    def check(self):
+        """The header / layout checks of the upload (ccdgpu_encoded_check; no device needed):
+        raises CcdGpuError naming the first problem."""
+        _check(lib().ccdgpu_encoded_check(self.n_chips, self.n_pix.ctypes.data, self.n_obs.ctypes.data,
+                                          self.buf.ctypes.data, int(self.nbytes_encoded)))
 
     def chip_modes(self):
         """Per chip: 1 if encoded, 0 if sent raw (from the section headers)."""
@@ -558,6 +574,49 @@ class Context(object):
             _check(rc)
         return rc == 1
 
+    def run_slot_begin_rows(self, slot, cx, cy, bufs, width=100):
+        """run_slot_begin with the batch's rows in the same device chain
+        (ccdgpu_run_slot_begin_rows): chip c's rows at (cx[c], cy[c]) land in ``bufs`` (a
+        RowsBuffers, grown here to the slot's pixels: offsets, mask words, and rows for
+        ``rows_per_pixel`` per pixel); run_slot_end_rows() waits once and returns them."""
+        batch = self._slot_keep.get(int(slot)) if hasattr(self, '_slot_keep') else None
+        if not isinstance(batch, ChipBatch):
+            raise ValueError('run_slot_begin_rows needs a stage_slot_chips / stage_slot_encoded batch')
+        cx = np.ascontiguousarray(cx, dtype=np.int32)
+        cy = np.ascontiguousarray(cy, dtype=np.int32)
+        if cx.shape != (batch.n_chips,) or cy.shape != (batch.n_chips,):
+            raise ValueError('cx / cy need one entry per chip (%d)' % batch.n_chips)
+        n_pix = int(batch.pix_off[-1])
+        words = (int(batch.n_obs.max()) + 31) // 32
+        bufs.ensure(n_pix + 1, int(bufs.rows_per_pixel * n_pix) + 64, n_pix * words)
+        _check(lib().ccdgpu_run_slot_begin_rows(self._ctx, int(slot), cx.ctypes.data, cy.ctypes.data, int(width),
+                                                bufs.offsets.ctypes.data, bufs.offsets.size, bufs.rows.ctypes.data,
+                                                bufs.rows.size, bufs.mask.ctypes.data, bufs.mask.size))
+        self._pending_slot = int(slot)
+        self._rows_req = (cx, cy, bufs, int(width), n_pix, words)
+
+    def run_slot_end_rows(self):
+        """(row_offsets [n_pix+1], rows, mask words [n_pix][words]) of the batch begun with
+        run_slot_begin_rows -- views of its RowsBuffers, valid until their next use.  More rows
+        than the buffer held: the buffer grows (and learns the rate) and the rows are fetched."""
+        secs = ctypes.c_double(0.0)
+        nr = ctypes.c_int64(0)
+        rc = lib().ccdgpu_run_slot_end_rows(self._ctx, ctypes.byref(secs), ctypes.byref(nr))
+        cx, cy, bufs, width, n_pix, words = self._rows_req
+        self._rows_req = None
+        self._keep = self._slot_keep.get(self._pending_slot)
+        self._n_pix = None
+        if rc == abi.E_OVERFLOW and nr.value > 0 and self._keep is not None and \
+                nr.value > bufs.rows.size and 'rows' in last_error():
+            bufs.rows_per_pixel = max(bufs.rows_per_pixel, 1.25 * nr.value / max(1, n_pix))
+            self.qa_error = False
+            return self.fetch_batch_rows_into(cx, cy, bufs, width)
+        if rc not in (0, abi.E_QA):
+            _check(rc)
+        self.qa_error = rc == abi.E_QA
+        n = nr.value
+        return bufs.offsets[:n_pix + 1], bufs.rows[:n], bufs.mask[:n_pix * words].reshape(n_pix, words)
+
     def run_slot_end(self):
         secs = ctypes.c_double(0.0)
         rc = lib().ccdgpu_run_slot_end(self._ctx, ctypes.byref(secs))
@@ -676,8 +735,9 @@ class RowsBuffers(object):
     """Reusable (pinned) landing buffers of Context.fetch_batch_rows_into: row offsets, rows
     (abi.ROW_DTYPE) and mask words; grown on demand, 25 % headroom."""
 
-    def __init__(self, pinned=True):
+    def __init__(self, pinned=True, rows_per_pixel=2.0):
         self.pinned = pinned
+        self.rows_per_pixel = float(rows_per_pixel)  # rows room of a batch chain (run_slot_begin_rows)
         self.offsets = np.zeros(0, np.int64)
         self.rows = np.zeros(0, abi.ROW_DTYPE)
         self.mask = np.zeros(0, np.uint32)

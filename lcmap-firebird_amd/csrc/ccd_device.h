@@ -102,6 +102,12 @@ int ccdk_decode_enc(const unsigned char *enc, int64_t total_pix, int16_t *spectr
 int ccdk_pack_rows(const ccdgpu_segment *seg, const int64_t *seg_off, const int64_t *row_off, const uint32_t *mask_bits,
                    int32_t mask_words, int32_t n_pix, int32_t n_obs, int32_t cx, int32_t cy, int32_t width,
                    ccdgpu_row *rows, int8_t *mask, void *stream);
+// the batch chain of ccdgpu_run_slot_begin_rows (ccd_rows.hip): pool -> CSR with the segment
+// count read on the device (counters[1], at most cap); rows per pixel for the row-offset scan
+int ccdk_scatter_dev(const ccdgpu_segment *pool, const int32_t *pool_seq, const unsigned long long *n_pool_dev,
+                     int64_t cap, const int64_t *offsets, const int64_t *chip_pix_off, int32_t n_chips,
+                     ccdgpu_segment *out, void *stream);
+int ccdk_row_counts(const int32_t *nseg, int64_t *offsets, int64_t n_pix, int64_t *rc, void *stream);
 // pool -> CSR; the segment's pixel field becomes the pixel index within its chip
 int ccdk_scatter(const ccdgpu_segment *pool, const int32_t *pool_seq, int64_t n_pool,
                  const int64_t *offsets, const int64_t *chip_pix_off, int32_t n_chips, ccdgpu_segment *out,

@@ -9,6 +9,7 @@
 // float cast) and the pixel table's processing mask as one byte per date (sorted order), so the
 // host only formats the ISO day strings.
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "../../include/ccdgpu.h"
@@ -69,7 +70,61 @@ __global__ __launch_bounds__(256) void ccd_pack_rows(const ccdgpu_segment *__res
     }
 }
 
+// Pool -> CSR with the segment count read on the device (counters[1] of the detection, for the
+// batch chain that is enqueued before the count is known): grid-stride over the pooled segments,
+// one wave per segment, its dwords copied lane-parallel; the pixel field becomes the pixel index
+// within its chip (the same result as ccd_scatter in ccd_kernels.hip).
+__global__ __launch_bounds__(256) void ccd_scatter_dev(const ccdgpu_segment *__restrict__ pool, const int32_t *__restrict__ seq,
+                                                       const unsigned long long *__restrict__ n_pool_dev, int64_t cap,
+                                                       const int64_t *__restrict__ offsets, const int64_t *__restrict__ chip_pix_off,
+                                                       int n_chips, ccdgpu_segment *__restrict__ out) {
+    const int64_t n = (int64_t)(*n_pool_dev < (unsigned long long)cap ? *n_pool_dev : (unsigned long long)cap);
+    const int l = threadIdx.x % W;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x / W);
+    for (int64_t s = (int64_t)blockIdx.x * (blockDim.x / W) + threadIdx.x / W; s < n; s += nw) {
+        const int gp = pool[s].pixel;
+        int lo = 0, hi = n_chips - 1;  // chip of the pixel
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (chip_pix_off[mid] <= gp) lo = mid;
+            else hi = mid - 1;
+        }
+        const int64_t dst = offsets[gp] + seq[s];
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(pool + s);
+        uint32_t *dd = reinterpret_cast<uint32_t *>(out + dst);
+        constexpr int NW = (int)(sizeof(ccdgpu_segment) / 4);
+        constexpr int PIXW = (int)(offsetof(ccdgpu_segment, pixel) / 4);
+        for (int i = l; i < NW; i += W) dd[i] = (i == PIXW) ? (uint32_t)(gp - chip_pix_off[lo]) : src[i];
+    }
+}
+
+// Rows per pixel (max(1, segments): pyccd.default's row for a pixel without a change model) with
+// a trailing zero, for the exclusive scan into row offsets; and the CSR offsets' closing entry.
+__global__ __launch_bounds__(256) void ccd_row_counts(const int32_t *__restrict__ nseg, int64_t *__restrict__ offsets,
+                                                      int64_t n_pix, int64_t *__restrict__ rc) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n_pix) rc[i] = nseg[i] > 0 ? nseg[i] : 1;
+    if (i == n_pix) {
+        rc[n_pix] = 0;
+        offsets[n_pix] = n_pix > 0 ? offsets[n_pix - 1] + nseg[n_pix - 1] : 0;
+    }
+}
+
 }  // namespace
+
+extern "C" int ccdk_scatter_dev(const ccdgpu_segment *pool, const int32_t *pool_seq, const unsigned long long *n_pool_dev,
+                                int64_t cap, const int64_t *offsets, const int64_t *chip_pix_off, int32_t n_chips,
+                                ccdgpu_segment *out, void *stream) {
+    hipLaunchKernelGGL(ccd_scatter_dev, dim3(256), dim3(256), 0, (hipStream_t)stream, pool, pool_seq, n_pool_dev, cap,
+                       offsets, chip_pix_off, n_chips, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int ccdk_row_counts(const int32_t *nseg, int64_t *offsets, int64_t n_pix, int64_t *rc, void *stream) {
+    const int64_t blocks = (n_pix + 1 + 255) / 256;
+    hipLaunchKernelGGL(ccd_row_counts, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, nseg, offsets, n_pix, rc);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 extern "C" int ccdk_pack_rows(const ccdgpu_segment *seg, const int64_t *seg_off, const int64_t *row_off,
                               const uint32_t *mask_bits, int32_t mask_words, int32_t n_pix, int32_t n_obs, int32_t cx,

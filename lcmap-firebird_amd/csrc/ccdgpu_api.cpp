@@ -246,6 +246,18 @@ struct ccdgpu_ctx {
     bool pending = false;
     int32_t pend_slot = -1;  // the upload slot that detection reads (not to be restaged until it ends)
     CcdDetectArgs pend_args{};
+    // the batch chain of ccdgpu_run_slot_begin_rows: CSR, row packing and the copies of rows,
+    // row offsets and mask words into the caller's (pinned) buffers, enqueued behind the
+    // detection; `done_rows` marks the end of the chain
+    bool rows_mode = false;
+    int64_t *rq_offsets = nullptr, *rq_seg = nullptr;
+    ccdgpu_row *rq_rows = nullptr;
+    uint32_t *rq_mask = nullptr;
+    int64_t rq_offsets_cap = 0, rq_rows_cap = 0, rq_mask_cap = 0;
+    int32_t rq_width = 100;
+    std::vector<int32_t> rq_cx, rq_cy;
+    DevBuf<int64_t> rowcnt;
+    hipEvent_t done_rows = nullptr;
     ~ccdgpu_ctx() {
         for (auto *b : {&dates, &sdates, &offsets, &chip_obs_off, &chip_pix_off, &chip_data_off, &row_off, &seg_off1, &b64_off})
             b->release();
@@ -281,6 +293,8 @@ struct ccdgpu_ctx {
         for (auto &e : ev)
             if (e) (void)hipEventDestroy(e);
         if (done) (void)hipEventDestroy(done);
+        if (done_rows) (void)hipEventDestroy(done_rows);
+        rowcnt.release();
         if (stream) (void)hipStreamDestroy(stream);
         release_arg_slot(arg_slot);
     }
@@ -420,6 +434,7 @@ int ccdgpu_init_copy_cus(int device, int copy_cus, ccdgpu_ctx **out) {
     }
     for (auto &e : c->ev) (void)hipEventCreate(&e);
     (void)hipEventCreateWithFlags(&c->done, hipEventBlockingSync | hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&c->done_rows, hipEventBlockingSync | hipEventDisableTiming);
     if ((masked ? hipExtStreamCreateWithCUMask(&c->copy_stream, (uint32_t)mask_copy.size(), mask_copy.data())
                 : hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking)) != hipSuccess) {
         delete c;
@@ -445,6 +460,17 @@ int ccdgpu_init_copy_cus(int device, int copy_cus, ccdgpu_ctx **out) {
             return fail(CCDGPU_EHIP, "hipStreamCreate failed");
         }
         c->aux_own = true;
+    } else if (const char *v = std::getenv("CCDGPU_AUX_PRIORITY")) {
+        // no CUs reserved: the launch's other kernels on a high-priority stream of their own, so the
+        // dispatcher serves them ahead of waiting detection waves (experiment knob)
+        if (std::atoi(v) != 0) {
+            int lo = 0, hi = 0;
+            if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
+                hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, hi) == hipSuccess)
+                c->aux_own = true;
+            else
+                c->aux = c->stream;
+        }
     }
     c->arg_slot = acquire_arg_slot();
     if (c->arg_slot < 0) {
@@ -681,18 +707,9 @@ int ccdgpu_stage_slot_chips(ccdgpu_ctx *c, int32_t slot, const ccdgpu_params *pa
     return 0;
 }
 
-int ccdgpu_stage_slot_encoded(ccdgpu_ctx *c, int32_t slot, const ccdgpu_params *params, int32_t n_chips,
-                              const int32_t *n_pix, const int32_t *n_obs, const int64_t *dates, const uint8_t *enc,
-                              int64_t enc_bytes) {
-    if (!c) return fail(CCDGPU_EINVAL, "NULL ctx");
-    if (slot < 0 || slot >= CCDGPU_UPLOAD_SLOTS)
-        return fail(CCDGPU_EINVAL, "slot must be in 0 .. " + std::to_string(CCDGPU_UPLOAD_SLOTS - 1));
-    if (c->pending && slot == c->pend_slot)
-        return fail(CCDGPU_EINVAL, "slot " + std::to_string(slot) + " is read by the detection begun with ccdgpu_run_slot_begin");
-    if (!dates || !enc) return fail(CCDGPU_EINVAL, "NULL input buffer");
-    Shape sh;
-    int rc = make_shape(n_chips, n_pix, n_obs, sh);
-    if (rc || (rc = check_params(params))) return rc;
+int ccdgpu_encoded_check(int32_t n_chips, const int32_t *n_pix, const int32_t *n_obs, const uint8_t *enc,
+                         int64_t enc_bytes) {
+    if (!enc || !n_pix || !n_obs || n_chips <= 0) return fail(CCDGPU_EINVAL, "NULL or empty encoded batch");
     // the encoded batch must describe exactly these chips (the decoder trusts its headers)
     const int64_t *tab = reinterpret_cast<const int64_t *>(enc);
     if (enc_bytes < (int64_t)(8 * (2 * (int64_t)n_chips + 3)) || tab[0] != n_chips)
@@ -701,6 +718,8 @@ int ccdgpu_stage_slot_encoded(ccdgpu_ctx *c, int32_t slot, const ccdgpu_params *
     if (off[n_chips] > enc_bytes) return fail(CCDGPU_EINVAL, "encoded batch: longer than enc_bytes");
     int64_t pb = 0, db = 0;
     for (int32_t k = 0; k < n_chips; ++k) {
+        if (n_pix[k] <= 0 || n_obs[k] <= 0 || n_obs[k] > CCDGPU_MAX_OBS)
+            return fail(CCDGPU_EINVAL, "encoded batch: chip " + std::to_string(k) + " has no pixels / observations");
         if (off[k] < 0 || off[k] + 128 > off[k + 1] || pixo[k] != pb)
             return fail(CCDGPU_EINVAL, "encoded batch: bad chip table entry " + std::to_string(k));
         const int32_t *h = reinterpret_cast<const int32_t *>(enc + off[k]);
@@ -730,6 +749,24 @@ int ccdgpu_stage_slot_encoded(ccdgpu_ctx *c, int32_t slot, const ccdgpu_params *
         db += (int64_t)n_pix[k] * n_obs[k];
     }
     if (pixo[n_chips] != pb) return fail(CCDGPU_EINVAL, "encoded batch: pixel total does not match");
+    return 0;
+}
+
+int ccdgpu_stage_slot_encoded(ccdgpu_ctx *c, int32_t slot, const ccdgpu_params *params, int32_t n_chips,
+                              const int32_t *n_pix, const int32_t *n_obs, const int64_t *dates, const uint8_t *enc,
+                              int64_t enc_bytes) {
+    if (!c) return fail(CCDGPU_EINVAL, "NULL ctx");
+    if (slot < 0 || slot >= CCDGPU_UPLOAD_SLOTS)
+        return fail(CCDGPU_EINVAL, "slot must be in 0 .. " + std::to_string(CCDGPU_UPLOAD_SLOTS - 1));
+    if (c->pending && slot == c->pend_slot)
+        return fail(CCDGPU_EINVAL, "slot " + std::to_string(slot) + " is read by the detection begun with ccdgpu_run_slot_begin");
+    if (!dates || !enc) return fail(CCDGPU_EINVAL, "NULL input buffer");
+    Shape sh;
+    int rc = make_shape(n_chips, n_pix, n_obs, sh);
+    if (rc || (rc = check_params(params))) return rc;
+    if ((rc = ccdgpu_encoded_check(n_chips, n_pix, n_obs, enc, enc_bytes))) return rc;
+    const int64_t *off = reinterpret_cast<const int64_t *>(enc) + 1;
+    const int64_t pb = sh.total_pix();
     HIPCHK(hipSetDevice(c->device));
     const size_t tobs = (size_t)sh.total_obs(), tdata = (size_t)sh.total_data();
     if ((rc = c->slot_dates[slot].ensure(tobs)) || (rc = c->slot_enc[slot].ensure((size_t)off[n_chips])))
@@ -786,7 +823,7 @@ int ccdgpu_run_slot(ccdgpu_ctx *c, int32_t slot, double *kernel_seconds) {
 
 static void detect_args(ccdgpu_ctx *c, CcdDetectArgs &a);
 static int launch(ccdgpu_ctx *c, CcdDetectArgs &a);
-static int finish(ccdgpu_ctx *c, double *kernel_seconds, bool *again);
+static int finish(ccdgpu_ctx *c, double *kernel_seconds, bool *again, bool chained = false);
 
 int ccdgpu_run_slot_begin(ccdgpu_ctx *c, int32_t slot) {
     int rc = slot_inputs(c, slot);
@@ -802,7 +839,7 @@ int ccdgpu_run_slot_begin(ccdgpu_ctx *c, int32_t slot) {
 int ccdgpu_run_query(ccdgpu_ctx *c) {
     if (!c) return fail(CCDGPU_EINVAL, "NULL ctx");
     if (!c->pending) return 1;
-    const hipError_t e = hipEventQuery(c->done);
+    const hipError_t e = hipEventQuery(c->rows_mode ? c->done_rows : c->done);
     if (e == hipSuccess) return 1;
     if (e == hipErrorNotReady) return 0;
     return fail(CCDGPU_EHIP, std::string("hipEventQuery: ") + hipGetErrorString(e));
@@ -811,6 +848,7 @@ int ccdgpu_run_query(ccdgpu_ctx *c) {
 int ccdgpu_run_slot_end(ccdgpu_ctx *c, double *kernel_seconds) {
     if (!c) return fail(CCDGPU_EINVAL, "NULL ctx");
     if (!c->pending) return fail(CCDGPU_EINVAL, "no detection begun with ccdgpu_run_slot_begin");
+    if (c->rows_mode) return fail(CCDGPU_EINVAL, "a detection begun with ccdgpu_run_slot_begin_rows ends with ccdgpu_run_slot_end_rows");
     HIPCHK(hipSetDevice(c->device));
     c->pending = false;
     c->pend_slot = -1;
@@ -821,6 +859,112 @@ int ccdgpu_run_slot_end(ccdgpu_ctx *c, double *kernel_seconds) {
         if (int rc2 = launch(c, c->pend_args)) return rc2;
     }
     return fail(CCDGPU_EOVERFLOW, "segment pool kept overflowing");
+}
+
+// The rest of a batch behind its detection, all on the aux stream (which already waits for the
+// detection's end): CSR offsets (scan), the closing entry and rows per pixel, row offsets
+// (scan), pool -> CSR with the device's segment count, row packing per chip, then the copies of
+// the CSR offsets (pinned staging), row offsets, rows (up to the caller's capacity) and mask
+// words into the caller's buffers.  Capacities are sized for any segment count the pool holds.
+static int enqueue_rows(ccdgpu_ctx *c) {
+    const Shape &sh = c->shape;
+    const int nc = sh.n_chips();
+    const int64_t np = c->total_pix;
+    hipStream_t ax = c->aux;
+    int rc;
+    const int64_t rows_dev = np + c->pool_cap;  // rows <= pixels + segments
+    if ((rc = c->csr.ensure(c->pool_cap > 0 ? c->pool_cap : 1)) || (rc = c->rows.ensure((size_t)rows_dev)) ||
+        (rc = c->row_off.ensure(np + 1)) || (rc = c->rowcnt.ensure(np + 1)) || (rc = c->offsets.ensure(np + 1)) ||
+        (rc = c->h_off.ensure(sizeof(int64_t) * (size_t)(np + 1))))
+        return rc;
+    size_t tmp_bytes = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, c->rowcnt.p, c->row_off.p, (int)np + 1, ax));
+    if ((rc = c->cub_tmp.ensure(tmp_bytes))) return rc;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->cub_tmp.p, tmp_bytes, c->nseg.p, c->offsets.p, (int)np, ax));
+    if (ccdk_row_counts(c->nseg.p, c->offsets.p, np, c->rowcnt.p, ax)) return fail(CCDGPU_EHIP, "row count launch failed");
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->cub_tmp.p, tmp_bytes, c->rowcnt.p, c->row_off.p, (int)np + 1, ax));
+    if (ccdk_scatter_dev(c->pool.p, c->pool_seq.p, c->counters.p + 1, c->pool_cap, c->offsets.p, c->chip_pix_off.p, nc,
+                         c->csr.p, ax))
+        return fail(CCDGPU_EHIP, "scatter launch failed");
+    for (int32_t ch = 0; ch < nc; ++ch) {
+        const int64_t q = sh.pix_off[ch];
+        if (ccdk_pack_rows(c->csr.p, c->offsets.p + q, c->row_off.p + q, c->mask.p + (size_t)q * c->mask_words,
+                           c->mask_words, sh.npix[ch], sh.nobs[ch], c->rq_cx[ch], c->rq_cy[ch], c->rq_width, c->rows.p,
+                           nullptr, ax))
+            return fail(CCDGPU_EHIP, "row packing launch failed");
+    }
+    const size_t ob = sizeof(int64_t) * (size_t)(np + 1);
+    HIPCHK(hipMemcpyAsync(c->h_off.p, c->offsets.p, ob, hipMemcpyDeviceToHost, ax));
+    HIPCHK(hipMemcpyAsync(c->rq_offsets, c->row_off.p, ob, hipMemcpyDeviceToHost, ax));
+    const int64_t nrc = std::min<int64_t>(c->rq_rows_cap, rows_dev);
+    if (nrc > 0) HIPCHK(hipMemcpyAsync(c->rq_rows, c->rows.p, sizeof(ccdgpu_row) * (size_t)nrc, hipMemcpyDeviceToHost, ax));
+    const size_t nbits = (size_t)np * c->mask_words;
+    if (nbits > 0) HIPCHK(hipMemcpyAsync(c->rq_mask, c->mask.p, sizeof(uint32_t) * nbits, hipMemcpyDeviceToHost, ax));
+    HIPCHK(hipEventRecord(c->done_rows, ax));
+    return 0;
+}
+
+int ccdgpu_run_slot_begin_rows(ccdgpu_ctx *c, int32_t slot, const int32_t *cx, const int32_t *cy, int32_t width,
+                               int64_t *row_offsets, int64_t offsets_cap, ccdgpu_row *rows, int64_t rows_cap,
+                               uint32_t *mask_bits, int64_t mask_cap) {
+    if (!c || !cx || !cy || !row_offsets || !rows || !mask_bits) return fail(CCDGPU_EINVAL, "NULL argument");
+    if (width <= 0) return fail(CCDGPU_EINVAL, "width must be > 0");
+    if (c->pending) return fail(CCDGPU_EINVAL, "a detection begun with ccdgpu_run_slot_begin is not finished");
+    if (slot < 0 || slot >= CCDGPU_UPLOAD_SLOTS || !c->slot_ready[slot]) return fail(CCDGPU_EINVAL, "slot has no staged batch");
+    const Shape &ssh = c->slot_shape[slot];
+    const int64_t np = ssh.total_pix();
+    const int64_t words = (ssh.n_obs_max + 31) / 32;
+    if (offsets_cap < np + 1 || mask_cap < np * words)
+        return fail(CCDGPU_EINVAL, "run_slot_begin_rows: offsets / mask buffers too small (need " + std::to_string(np + 1) +
+                                       " offsets, " + std::to_string(np * words) + " mask words)");
+    int rc = slot_inputs(c, slot);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(c->device));
+    c->rq_offsets = row_offsets;
+    c->rq_offsets_cap = offsets_cap;
+    c->rq_rows = rows;
+    c->rq_rows_cap = rows_cap;
+    c->rq_mask = mask_bits;
+    c->rq_mask_cap = mask_cap;
+    c->rq_width = width;
+    const int nc = c->shape.n_chips();
+    c->rq_cx.assign(cx, cx + nc);
+    c->rq_cy.assign(cy, cy + nc);
+    detect_args(c, c->pend_args);
+    if ((rc = launch(c, c->pend_args)) || (rc = enqueue_rows(c))) return rc;
+    c->pending = true;
+    c->rows_mode = true;
+    c->pend_slot = slot;
+    return 0;
+}
+
+int ccdgpu_run_slot_end_rows(ccdgpu_ctx *c, double *kernel_seconds, int64_t *n_rows) {
+    if (!c) return fail(CCDGPU_EINVAL, "NULL ctx");
+    if (n_rows) *n_rows = 0;
+    if (!c->pending || !c->rows_mode) return fail(CCDGPU_EINVAL, "no detection begun with ccdgpu_run_slot_begin_rows");
+    HIPCHK(hipSetDevice(c->device));
+    c->pending = false;
+    c->rows_mode = false;
+    c->pend_slot = -1;
+    int rc = 0;
+    for (int attempt = 0;; ++attempt) {
+        HIPCHK(hipEventSynchronize(c->done_rows));
+        bool again = false;
+        rc = finish(c, kernel_seconds, &again, true);
+        if (!again) break;
+        if (attempt == 3) return fail(CCDGPU_EOVERFLOW, "segment pool kept overflowing");
+        int rc2;
+        if ((rc2 = launch(c, c->pend_args)) || (rc2 = enqueue_rows(c))) return rc2;
+    }
+    if (rc && rc != CCDGPU_EQA) return rc;
+    const int64_t nr = c->rq_offsets[c->total_pix];
+    if (n_rows) *n_rows = nr;
+    if (nr > c->rq_rows_cap) {
+        // the run is complete (ccdgpu_fetch_batch_rows_into fetches it into larger buffers)
+        return fail(CCDGPU_EOVERFLOW, "run_slot_end_rows: " + std::to_string(nr) + " rows, the buffer holds " +
+                                          std::to_string(c->rq_rows_cap));
+    }
+    return rc;
 }
 
 int ccdgpu_staged_inputs(ccdgpu_ctx *c, int16_t *spectra, uint16_t *qa) {
@@ -926,7 +1070,7 @@ static int launch(ccdgpu_ctx *c, CcdDetectArgs &a) {
     return 0;
 }
 
-static int finish(ccdgpu_ctx *c, double *kernel_seconds, bool *again) {
+static int finish(ccdgpu_ctx *c, double *kernel_seconds, bool *again, bool chained) {
     const ccdgpu_params &p = c->params;
     const Shape &sh = c->shape;
     const int nc = sh.n_chips();
@@ -934,7 +1078,9 @@ static int finish(ccdgpu_ctx *c, double *kernel_seconds, bool *again) {
     unsigned long long *h = reinterpret_cast<unsigned long long *>(c->h_small.p + 64);
     unsigned long long *hst = reinterpret_cast<unsigned long long *>(c->h_small.p + 128);
     *again = false;
-    if (c->done) {
+    if (chained) {
+        // the batch chain has completed (the caller waited for done_rows)
+    } else if (c->done) {
         HIPCHK(hipEventSynchronize(c->done));
     } else {
         HIPCHK(hipStreamSynchronize(ax));
@@ -967,8 +1113,13 @@ static int finish(ccdgpu_ctx *c, double *kernel_seconds, bool *again) {
     (void)hipEventElapsedTime(&ms_det, c->ev[1], c->ev[2]);
     const unsigned long long *st = hst;
     for (int i = 0; i < CCD_NSTATS; ++i) c->diag[i] = st[i];
-    // CSR: exclusive scan of per-pixel counts, then scatter the pool
     int rc;
+    if (chained) {
+        // CSR, offsets and rows were made by the chain (enqueue_rows); the offsets are in h_off
+        c->h_offsets.resize(c->total_pix + 1);
+        std::memcpy(c->h_offsets.data(), c->h_off.p, sizeof(int64_t) * (size_t)(c->total_pix + 1));
+    } else {
+    // CSR: exclusive scan of per-pixel counts, then scatter the pool
     if ((rc = c->csr.ensure(c->n_pool > 0 ? c->n_pool : 1))) return rc;
     size_t tmp_bytes = 0;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, c->nseg.p, c->offsets.p, (int)c->total_pix + 1, ax));
@@ -985,6 +1136,7 @@ static int finish(ccdgpu_ctx *c, double *kernel_seconds, bool *again) {
         return fail(CCDGPU_EHIP, "scatter launch failed");
     HIPCHK(hipEventRecord(c->ev[3], ax));
     HIPCHK(hipStreamSynchronize(ax));
+    }
     c->last.detect_ms = ms_det;
     c->last.detect_ms_device = h[6] > h[5] ? (double)(h[6] - h[5]) / 1e5 : 0.0;  // 100 MHz clock
     c->last.prep_ms = ms_prep;

@@ -177,3 +177,37 @@ def test_scalar_encoder_dropped_last_observation_at_thread_boundaries():
     keep[[4, n - 1]] = False
     np.testing.assert_array_equal(ds[:, :, keep], s[:, :, keep])
     assert (ds[:, :, ~keep] == -9999).all()
+
+
+def test_encoded_check_rejects_malformed_batches_on_the_host():
+    """ccdgpu_encoded_check (the checks ccdgpu_stage_slot_encoded makes before the upload; no
+    device): a band stride below the kept count or not a multiple of 8, a kept-offset table that
+    does not end at kept or is not monotone, a kept count past the chip, a truncated section and a
+    shape mismatch are rejected; the intact batch passes."""
+    cs = [synth.chip(synth.config(3), 0, 0, 64), synth.chip(synth.config(3), 1, 0, 40)]
+    e, _ = encode(cs, threads=2)
+    assert e.chip_modes() == [1, 1]
+    e.check()
+    off = [int(o) for o in e.buf[8:8 * (e.n_chips + 2)].view(np.int64)]
+
+    def corrupt(fn):
+        import copy
+        b = copy.copy(e)
+        b.buf = e.buf.copy()
+        fn(b)
+        with pytest.raises(ccdgpu.CcdGpuError, match='encoded batch'):
+            b.check()
+
+    def h64(b, k):
+        return b.buf[off[k] + 48:off[k] + 80].view(np.int64)
+
+    def koff(b, k, n):
+        return b.buf[off[k] + 128:off[k] + 128 + 4 * (n + 1)].view(np.uint32)
+
+    corrupt(lambda b: h64(b, 0).__setitem__(2, h64(b, 0)[0] - 8))
+    corrupt(lambda b: h64(b, 0).__setitem__(2, h64(b, 0)[2] + 4))
+    corrupt(lambda b: koff(b, 1, 40).__setitem__(40, koff(b, 1, 40)[40] - 1))
+    corrupt(lambda b: koff(b, 0, 64).__setitem__(slice(3, 5), [koff(b, 0, 64)[4] + 1, koff(b, 0, 64)[3]]))
+    corrupt(lambda b: h64(b, 0).__setitem__(slice(0, 3, 2), [64 * 1421 * 2, 64 * 1421 * 2]))
+    corrupt(lambda b: setattr(b, 'nbytes_encoded', off[2] - 64))
+    corrupt(lambda b: b.buf[off[1] + 4:off[1] + 8].view(np.int32).__setitem__(0, 41))

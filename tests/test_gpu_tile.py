@@ -138,3 +138,34 @@ def test_full_size_tile_with_product_defaults_matches_oracle_on_stratified_pixel
     print('full-size tile parity: %s, runner %.1f s' % (out, run_s))
     assert out['pixels'] >= 100 * FULL_CHIPS - 5 and out['chips'] == FULL_CHIPS
     assert out['int_mismatches'] == 0 and out['float_mismatches'] == 0, out
+
+
+def test_batch_chain_rows_equal_the_fetched_rows_and_overflow_falls_back():
+    """ccdgpu_run_slot_begin_rows / _end_rows (the rows in the detection's device chain) give the
+    rows, offsets and mask words of run_slot + fetch_batch_rows_into, byte for byte; with a rows
+    buffer too small for the batch (C5 chips: several segments per pixel) the run completes,
+    reports the count and the rows are fetched into the grown buffer."""
+    import ccdgpu
+    from ccdgpu import synth
+    cs = [synth.chip(synth.config(5), 3, 0, 400), synth.chip(synth.config(3), 4, 0, 300),
+          synth.chip(synth.config(3), 5, 0, 200)]
+    enc = ccdgpu.EncodedBatch.encode(cs, threads=4)
+    cx, cy = [-1815585, -1812585, -1809585], [1064805, 1064805, 1061805]
+    ctx = ccdgpu.Context(0, copy_cus=8)
+    try:
+        ctx.stage_slot_chips(0, enc)
+        ctx.run_slot(0)
+        ref = [np.array(a) for a in ctx.fetch_batch_rows_into(cx, cy, ccdgpu.RowsBuffers())]
+        for rpp in (2.0, 0.5):
+            bufs = ccdgpu.RowsBuffers(rows_per_pixel=rpp)
+            ctx.stage_slot_chips(1, enc)
+            ctx.run_slot_begin_rows(1, cx, cy, bufs)
+            got = ctx.run_slot_end_rows()
+            assert np.array_equal(got[0], ref[0]), rpp
+            assert got[1].tobytes() == ref[1].tobytes(), rpp
+            assert np.array_equal(got[2], ref[2]), rpp
+            if rpp < 1:
+                assert bufs.rows_per_pixel > rpp  # learned from the overflow
+    finally:
+        ctx.close()
+    assert ref[1].shape[0] > 900  # more rows than 0.5 per pixel

@@ -30,7 +30,13 @@ batch = bench.build_batch(cfg, ids)
 out = {}
 
 
-def trial(tag, n_ctx, copy_cus):
+chips = [batch.chip(c) for c in range(batch.n_chips)]
+drop, strict = ccdgpu.unread_drop_bits(None)
+encs = [ccdgpu.EncodedBatch.encode(chips, threads=8, drop_bits=drop, strict_bits=strict) for _ in range(3)]
+cx = [0] * batch.n_chips
+
+
+def trial(tag, n_ctx, copy_cus, mode='run'):
     ctxs = [ccdgpu.Context(0, copy_cus=copy_cus) for _ in range(n_ctx)]
     for c in ctxs:
         c.stage_chips(batch)
@@ -39,8 +45,18 @@ def trial(tag, n_ctx, copy_cus):
         c.synchronize()
 
     def go(c):
-        for _ in range(a.launches):
-            c.run()
+        bufs = ccdgpu.RowsBuffers()
+        for i in range(a.launches):
+            if mode == 'run':
+                c.run()
+            elif mode == 'fetch':
+                c.run()
+                c._keep = batch
+                c.fetch_batch_rows_into(cx, cx, bufs)
+            else:  # upload an encoded batch (pinned, prepared), detect, fetch rows
+                c.stage_slot_chips(i % 3, encs[i % 3])
+                c.run_slot(i % 3)
+                c.fetch_batch_rows_into(cx, cx, bufs)
 
     th = [threading.Thread(target=go, args=(c,)) for c in ctxs]
     t = time.perf_counter()
@@ -53,11 +69,11 @@ def trial(tag, n_ctx, copy_cus):
         c.close()
     rate = n_ctx * a.launches * batch.total_pixels / el
     out[tag] = rate
-    print('%-16s contexts %d copy_cus %d: %.0f px/s' % (tag, n_ctx, copy_cus, rate), flush=True)
+    print('%-16s contexts %d copy_cus %d mode %s: %.0f px/s' % (tag, n_ctx, copy_cus, mode, rate), flush=True)
 
 
-for cus in (0, 8):
-    for n in (1, 2, 4):
-        trial('n%d_cus%d' % (n, cus), n, cus)
+for mode in ('run', 'fetch', 'upload'):
+    for n in (1, 4):
+        trial('%s_n%d' % (mode, n), n, 8, mode)
 print(json.dumps({'per': a.per, 'launches': a.launches, 'rates': out,
                   'GPU_MAX_HW_QUEUES': os.environ.get('GPU_MAX_HW_QUEUES')}))
