@@ -129,3 +129,42 @@ class SplitOracleContext(OracleContext):
         self._pending = None
         self.run_slot(slot)
 
+
+
+class ChainOracleContext(SplitOracleContext):
+    """SplitOracleContext with the device context's batch chain (run_slot_begin_rows /
+    run_slot_end_rows): the rows land in the caller's RowsBuffers, whose rows room is learned
+    from an overflow exactly as ccdgpu.Context does (too small: the rows are fetched after)."""
+
+    def __init__(self, device=0, threads=2, run_time=0.05, **kw):
+        super(ChainOracleContext, self).__init__(device, threads, run_time, **kw)
+        self.chained = 0
+        self.overflowed = 0
+
+    def fetch_batch_rows_into(self, cx, cy, bufs, width=100):
+        off, rows, bits = self.fetch_batch_rows(cx, cy, width)
+        n_pix, words = bits.shape
+        bufs.ensure(off.size, rows.size, bits.size)
+        bufs.offsets[:off.size] = off
+        bufs.rows[:rows.size] = rows
+        bufs.mask[:bits.size] = bits.reshape(-1)
+        return bufs.offsets[:off.size], bufs.rows[:rows.size], bufs.mask[:bits.size].reshape(n_pix, words)
+
+    def run_slot_begin_rows(self, slot, cx, cy, bufs, width=100):
+        batch = self._slots[slot][0]
+        n_pix = int(batch.pix_off[-1])
+        words = (int(batch.n_obs.max()) + 31) // 32
+        bufs.ensure(n_pix + 1, int(bufs.rows_per_pixel * n_pix) + 64, n_pix * words)
+        self.run_slot_begin(slot)
+        self._rows_req = (np.array(cx), np.array(cy), bufs, width)
+
+    def run_slot_end_rows(self):
+        self.run_slot_end()
+        cx, cy, bufs, width = self._rows_req
+        self.chained += 1
+        cap = bufs.rows.size
+        off, rows, bits = self.fetch_batch_rows(cx, cy, width)
+        if rows.size > cap:
+            self.overflowed += 1
+            bufs.rows_per_pixel = max(bufs.rows_per_pixel, 1.25 * rows.size / max(1, off.size - 1))
+        return self.fetch_batch_rows_into(cx, cy, bufs, width)

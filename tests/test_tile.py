@@ -259,3 +259,33 @@ def test_one_tile_split_over_world4_with_a_slow_rank():
     assert sum(s['chips'] for s in st.values()) == 24
     assert st[3]['chips'] < max(st[r]['chips'] for r in (0, 1, 2))
     assert all('tail_seconds' in s and s['tail_seconds'] >= 0.0 for s in st.values())
+
+
+def test_tile_run_through_the_batch_chain_equals_the_plain_run():
+    """The runner's batch-chain path (run_slot_begin_rows / run_slot_end_rows, the device
+    context's default): every batch goes through the chain and the rows equal a plain run's (the
+    rows-buffer overflow of the chain is covered on the GPU, tests/test_gpu_tile.py)."""
+    import ccdgpu
+    from ccdc import runner
+    from rows_util import ChainOracleContext, OracleContext
+    made = []
+
+    def chain(dev):
+        made.append(ChainOracleContext(dev, threads=2, run_time=0.02))
+        return made[-1]
+
+    orig = ccdgpu.RowsBuffers.__init__
+
+    def small(self, pinned=True, rows_per_pixel=0.25):
+        orig(self, pinned=False, rows_per_pixel=rows_per_pixel)
+
+    ccdgpu.RowsBuffers.__init__ = small
+    try:
+        res = runner.changedetection(tile(), source, contexts=2, batch_chips=2, number=N_CHIPS, encode=False,
+                                     context_factory=chain)
+    finally:
+        ccdgpu.RowsBuffers.__init__ = orig
+    ref = runner.changedetection(tile(), source, contexts=1, batch_chips=3, number=N_CHIPS, encode=False,
+                                 context_factory=lambda dev: OracleContext(dev, threads=2))
+    assert [c['digest'] for c in res['chips']] == [c['digest'] for c in ref['chips']]
+    assert sum(c.chained for c in made) == sum(st['batches'] for st in res['ranks'])
