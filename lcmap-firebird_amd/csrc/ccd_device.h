@@ -99,14 +99,19 @@ int ccdk_unpack_b64(const unsigned char *text, int64_t text_bytes, const int64_t
 // transport-encoded batch (ccd_encode.c) -> spectra / qa in the standard layout (ccd_pack.hip)
 int ccdk_decode_enc(const unsigned char *enc, int64_t total_pix, int16_t *spectra, uint16_t *qa, void *stream);
 // detection results -> segment / pixel table rows (ccd_rows.hip)
+// (skip: nullptr, or a device flag that makes the launch write nothing; seg_cap / rows_cap bound
+// the segment reads and row writes)
 int ccdk_pack_rows(const ccdgpu_segment *seg, const int64_t *seg_off, const int64_t *row_off, const uint32_t *mask_bits,
                    int32_t mask_words, int32_t n_pix, int32_t n_obs, int32_t cx, int32_t cy, int32_t width,
-                   ccdgpu_row *rows, int8_t *mask, void *stream);
+                   ccdgpu_row *rows, int8_t *mask, const unsigned long long *skip, int64_t seg_cap, int64_t rows_cap,
+                   void *stream);
 // the batch chain of ccdgpu_run_slot_begin_rows (ccd_rows.hip): pool -> CSR with the segment
 // count read on the device (counters[1], at most cap); rows per pixel for the row-offset scan
+// (overflow: the detection's pool-overflow flag -- set, the chain's kernels write nothing and the
+// host reruns the batch with a larger pool)
 int ccdk_scatter_dev(const ccdgpu_segment *pool, const int32_t *pool_seq, const unsigned long long *n_pool_dev,
-                     int64_t cap, const int64_t *offsets, const int64_t *chip_pix_off, int32_t n_chips,
-                     ccdgpu_segment *out, void *stream);
+                     const unsigned long long *overflow, int64_t cap, const int64_t *offsets,
+                     const int64_t *chip_pix_off, int32_t n_chips, ccdgpu_segment *out, void *stream);
 int ccdk_row_counts(const int32_t *nseg, int64_t *offsets, int64_t n_pix, int64_t *rc, void *stream);
 // pool -> CSR; the segment's pixel field becomes the pixel index within its chip
 int ccdk_scatter(const ccdgpu_segment *pool, const int32_t *pool_seq, int64_t n_pool,

@@ -18,10 +18,16 @@ namespace {
 
 constexpr int W = 64;
 
+// skip: the detection's pool-overflow flag (batch chain: the segment counts then exceed what the
+// pool holds, and the host reruns the batch), nullptr when the host checked it first; seg_cap /
+// rows_cap bound every segment read and row write.
 __global__ __launch_bounds__(256) void ccd_pack_rows(const ccdgpu_segment *__restrict__ seg, const int64_t *__restrict__ seg_off,
                                                      const int64_t *__restrict__ row_off, const uint32_t *__restrict__ mask_bits,
                                                      int mask_words, int n_pix, int n_obs, int cx, int cy, int width,
-                                                     ccdgpu_row *__restrict__ rows, int8_t *__restrict__ mask) {
+                                                     ccdgpu_row *__restrict__ rows, int8_t *__restrict__ mask,
+                                                     const unsigned long long *__restrict__ skip, int64_t seg_cap,
+                                                     int64_t rows_cap) {
+    if (skip && *skip) return;
     const int wave = (int)(blockIdx.x * (blockDim.x / W) + threadIdx.x / W);
     const int l = threadIdx.x % W;
     const int nwaves = (int)(gridDim.x * (blockDim.x / W));
@@ -29,9 +35,12 @@ __global__ __launch_bounds__(256) void ccd_pack_rows(const ccdgpu_segment *__res
         const int64_t s0 = seg_off[p], s1 = seg_off[p + 1];
         const int64_t r0 = row_off[p];
         const int px = cx + 30 * (p % width), py = cy - 30 * (p / width);
+        // (offsets outside the segment array -- a batch chain after a pool overflow -- write nothing)
+        if (s1 < s0 || s0 < 0 || (s1 > s0 && s1 > seg_cap) || s1 - s0 > 4096 || r0 < 0 || r0 >= rows_cap) continue;
         const int ns = (int)(s1 - s0);
         // one lane per row; a pixel without change models gets pyccd.default's row
         for (int j = l; j < (ns > 0 ? ns : 1); j += W) {
+            if (r0 + j >= rows_cap || (ns > 0 && s0 + j >= seg_cap)) continue;
             ccdgpu_row r;
             r.px = px;
             r.py = py;
@@ -75,9 +84,11 @@ __global__ __launch_bounds__(256) void ccd_pack_rows(const ccdgpu_segment *__res
 // one wave per segment, its dwords copied lane-parallel; the pixel field becomes the pixel index
 // within its chip (the same result as ccd_scatter in ccd_kernels.hip).
 __global__ __launch_bounds__(256) void ccd_scatter_dev(const ccdgpu_segment *__restrict__ pool, const int32_t *__restrict__ seq,
-                                                       const unsigned long long *__restrict__ n_pool_dev, int64_t cap,
+                                                       const unsigned long long *__restrict__ n_pool_dev,
+                                                       const unsigned long long *__restrict__ overflow, int64_t cap,
                                                        const int64_t *__restrict__ offsets, const int64_t *__restrict__ chip_pix_off,
                                                        int n_chips, ccdgpu_segment *__restrict__ out) {
+    if (overflow && *overflow) return;  // the pool overflowed: the host reruns the batch
     const int64_t n = (int64_t)(*n_pool_dev < (unsigned long long)cap ? *n_pool_dev : (unsigned long long)cap);
     const int l = threadIdx.x % W;
     const int64_t nw = (int64_t)gridDim.x * (blockDim.x / W);
@@ -90,6 +101,7 @@ __global__ __launch_bounds__(256) void ccd_scatter_dev(const ccdgpu_segment *__r
             else hi = mid - 1;
         }
         const int64_t dst = offsets[gp] + seq[s];
+        if (dst < 0 || dst >= cap) continue;
         const uint32_t *src = reinterpret_cast<const uint32_t *>(pool + s);
         uint32_t *dd = reinterpret_cast<uint32_t *>(out + dst);
         constexpr int NW = (int)(sizeof(ccdgpu_segment) / 4);
@@ -113,10 +125,10 @@ __global__ __launch_bounds__(256) void ccd_row_counts(const int32_t *__restrict_
 }  // namespace
 
 extern "C" int ccdk_scatter_dev(const ccdgpu_segment *pool, const int32_t *pool_seq, const unsigned long long *n_pool_dev,
-                                int64_t cap, const int64_t *offsets, const int64_t *chip_pix_off, int32_t n_chips,
-                                ccdgpu_segment *out, void *stream) {
-    hipLaunchKernelGGL(ccd_scatter_dev, dim3(256), dim3(256), 0, (hipStream_t)stream, pool, pool_seq, n_pool_dev, cap,
-                       offsets, chip_pix_off, n_chips, out);
+                                const unsigned long long *overflow, int64_t cap, const int64_t *offsets,
+                                const int64_t *chip_pix_off, int32_t n_chips, ccdgpu_segment *out, void *stream) {
+    hipLaunchKernelGGL(ccd_scatter_dev, dim3(256), dim3(256), 0, (hipStream_t)stream, pool, pool_seq, n_pool_dev, overflow,
+                       cap, offsets, chip_pix_off, n_chips, out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -128,10 +140,11 @@ extern "C" int ccdk_row_counts(const int32_t *nseg, int64_t *offsets, int64_t n_
 
 extern "C" int ccdk_pack_rows(const ccdgpu_segment *seg, const int64_t *seg_off, const int64_t *row_off,
                               const uint32_t *mask_bits, int32_t mask_words, int32_t n_pix, int32_t n_obs, int32_t cx,
-                              int32_t cy, int32_t width, ccdgpu_row *rows, int8_t *mask, void *stream) {
+                              int32_t cy, int32_t width, ccdgpu_row *rows, int8_t *mask, const unsigned long long *skip,
+                              int64_t seg_cap, int64_t rows_cap, void *stream) {
     const int waves = n_pix < 4096 ? n_pix : 4096;
     const int blocks = (waves + 3) / 4;
     hipLaunchKernelGGL(ccd_pack_rows, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, (hipStream_t)stream, seg, seg_off,
-                       row_off, mask_bits, mask_words, n_pix, n_obs, cx, cy, width, rows, mask);
+                       row_off, mask_bits, mask_words, n_pix, n_obs, cx, cy, width, rows, mask, skip, seg_cap, rows_cap);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

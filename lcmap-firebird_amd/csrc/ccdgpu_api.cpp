@@ -10,6 +10,8 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <climits>
+#include <cstdint>
 #include <chrono>
 #include <cctype>
 #include <cmath>
@@ -877,20 +879,25 @@ static int enqueue_rows(ccdgpu_ctx *c) {
         (rc = c->row_off.ensure(np + 1)) || (rc = c->rowcnt.ensure(np + 1)) || (rc = c->offsets.ensure(np + 1)) ||
         (rc = c->h_off.ensure(sizeof(int64_t) * (size_t)(np + 1))))
         return rc;
-    size_t tmp_bytes = 0;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, c->rowcnt.p, c->row_off.p, (int)np + 1, ax));
-    if ((rc = c->cub_tmp.ensure(tmp_bytes))) return rc;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->cub_tmp.p, tmp_bytes, c->nseg.p, c->offsets.p, (int)np, ax));
+    // temporary storage of both scans (their instantiations differ: int32 counts -> int64 offsets,
+    // int64 row counts -> int64 row offsets), each called with its own size
+    size_t tmp_seg = 0, tmp_row = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_seg, c->nseg.p, c->offsets.p, (int)np, ax));
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_row, c->rowcnt.p, c->row_off.p, (int)np + 1, ax));
+    if ((rc = c->cub_tmp.ensure(std::max(tmp_seg, tmp_row)))) return rc;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->cub_tmp.p, tmp_seg, c->nseg.p, c->offsets.p, (int)np, ax));
     if (ccdk_row_counts(c->nseg.p, c->offsets.p, np, c->rowcnt.p, ax)) return fail(CCDGPU_EHIP, "row count launch failed");
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->cub_tmp.p, tmp_bytes, c->rowcnt.p, c->row_off.p, (int)np + 1, ax));
-    if (ccdk_scatter_dev(c->pool.p, c->pool_seq.p, c->counters.p + 1, c->pool_cap, c->offsets.p, c->chip_pix_off.p, nc,
-                         c->csr.p, ax))
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->cub_tmp.p, tmp_row, c->rowcnt.p, c->row_off.p, (int)np + 1, ax));
+    // (on a pool overflow -- counters[3] -- the segment counts exceed what the pool holds: the scatter
+    // and the row packing write nothing and ccdgpu_run_slot_end_rows reruns the batch)
+    if (ccdk_scatter_dev(c->pool.p, c->pool_seq.p, c->counters.p + 1, c->counters.p + 3, c->pool_cap, c->offsets.p,
+                         c->chip_pix_off.p, nc, c->csr.p, ax))
         return fail(CCDGPU_EHIP, "scatter launch failed");
     for (int32_t ch = 0; ch < nc; ++ch) {
         const int64_t q = sh.pix_off[ch];
         if (ccdk_pack_rows(c->csr.p, c->offsets.p + q, c->row_off.p + q, c->mask.p + (size_t)q * c->mask_words,
                            c->mask_words, sh.npix[ch], sh.nobs[ch], c->rq_cx[ch], c->rq_cy[ch], c->rq_width, c->rows.p,
-                           nullptr, ax))
+                           nullptr, c->counters.p + 3, c->pool_cap, rows_dev, ax))
             return fail(CCDGPU_EHIP, "row packing launch failed");
     }
     const size_t ob = sizeof(int64_t) * (size_t)(np + 1);
@@ -1268,7 +1275,7 @@ static int fetch_rows_range(ccdgpu_ctx *c, int32_t c0, int32_t c1, const int32_t
         const int64_t q = sh.pix_off[ch] - p0;
         if (ccdk_pack_rows(c->csr.p + s0, c->seg_off1.p + q, c->row_off.p + q, c->mask.p + (size_t)sh.pix_off[ch] * c->mask_words,
                            c->mask_words, sh.npix[ch], sh.nobs[ch], cx[ch - c0], cy[ch - c0], width, c->rows.p,
-                           packed_mask ? nullptr : c->mask8.p + (sh.data_off[ch] - d0), ax))
+                           packed_mask ? nullptr : c->mask8.p + (sh.data_off[ch] - d0), nullptr, INT64_MAX, INT64_MAX, ax))
             return fail(CCDGPU_EHIP, "row packing launch failed");
     }
     out->n_pix = (int32_t)np;
@@ -1366,7 +1373,8 @@ int ccdgpu_fetch_batch_rows_into(ccdgpu_ctx *c, const int32_t *cx, const int32_t
     for (int32_t ch = 0; ch < nc; ++ch) {
         const int64_t q = sh.pix_off[ch];
         if (ccdk_pack_rows(c->csr.p + s0, c->seg_off1.p + q, c->row_off.p + q, c->mask.p + (size_t)q * c->mask_words,
-                           c->mask_words, sh.npix[ch], sh.nobs[ch], cx[ch], cy[ch], width, c->rows.p, nullptr, ax))
+                           c->mask_words, sh.npix[ch], sh.nobs[ch], cx[ch], cy[ch], width, c->rows.p, nullptr, nullptr,
+                           INT64_MAX, INT64_MAX, ax))
             return fail(CCDGPU_EHIP, "row packing launch failed");
     }
     // straight into the caller's buffers (DMA when they are pinned: ccdgpu_host_alloc)
