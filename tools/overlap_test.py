@@ -15,6 +15,7 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, 'lcmap-firebird_amd')]
+import numpy as np  # noqa: E402
 import bench  # noqa: E402
 import ccdgpu  # noqa: E402
 from ccdgpu import synth  # noqa: E402
@@ -23,10 +24,20 @@ ap = argparse.ArgumentParser()
 ap.add_argument('--config', type=int, default=3)
 ap.add_argument('--per', type=int, default=8)
 ap.add_argument('--launches', type=int, default=12)
+ap.add_argument('--modes', default='run,fetch,upload')
+ap.add_argument('--pool', action='store_true',
+                help="the bench tile leg's chips (TileSource pool mode: date-shifted copies of GPU-generated chips, "
+                     "positions 0..per-1) instead of the resident leg's")
 a = ap.parse_args()
 cfg = synth.config(a.config)
-ids = bench.chip_ids(0, 64, 1, lambda c: bench.synth_nobs(cfg, c))[::64 // a.per][:a.per]
-batch = bench.build_batch(cfg, ids)
+if a.pool:
+    src = synth.TileSource(cfg, device=0, batch_chips=a.per, mode='pool', pool_chips=32)
+    src.prepare()
+    batch = ccdgpu.ChipBatch.from_chips([tuple(np.array(x) for x in v) for v in src.views(list(range(a.per)))])
+    src.close()
+else:
+    ids = bench.chip_ids(0, 64, 1, lambda c: bench.synth_nobs(cfg, c))[::64 // a.per][:a.per]
+    batch = bench.build_batch(cfg, ids)
 out = {}
 
 
@@ -72,8 +83,8 @@ def trial(tag, n_ctx, copy_cus, mode='run'):
     print('%-16s contexts %d copy_cus %d mode %s: %.0f px/s' % (tag, n_ctx, copy_cus, mode, rate), flush=True)
 
 
-for mode in ('run', 'fetch', 'upload'):
+for mode in a.modes.split(','):
     for n in (1, 4):
         trial('%s_n%d' % (mode, n), n, 8, mode)
-print(json.dumps({'per': a.per, 'launches': a.launches, 'rates': out,
+print(json.dumps({'per': a.per, 'launches': a.launches, 'pool': a.pool, 'rates': out,
                   'GPU_MAX_HW_QUEUES': os.environ.get('GPU_MAX_HW_QUEUES')}))
