@@ -222,3 +222,21 @@ def test_concurrent_contexts_on_one_device():
         assert np.array_equal(g.seg_offsets, r.seg_offsets)
         assert g.segments.tobytes() == r.segments.tobytes()
         assert np.array_equal(g.mask, r.mask)
+
+
+def test_cu_reservation_extremes_keep_both_stream_masks_nonempty():
+    """ccdgpu_init_copy_cus with a reservation near the CU count: every group of CUs keeps at least
+    one for the detection and reserves at least one (the reservation is clamped, never empty on
+    either side), and the detection is the unreserved one's."""
+    d, s, q = synth.chip(synth.config(3), 9, 0, 200)
+    ref = ccdgpu.Context(0)
+    r = ref.detect_batch(d, s, q)
+    ref.close()
+    for cus in (1, 255):
+        ctx = ccdgpu.Context(0, copy_cus=cus)
+        try:
+            g = ctx.detect_batch(d, s, q)
+        finally:
+            ctx.close()
+        assert g.segments.tobytes() == r.segments.tobytes(), cus
+        assert np.array_equal(g.mask, r.mask), cus
