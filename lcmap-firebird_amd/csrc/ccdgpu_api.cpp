@@ -163,11 +163,16 @@ int make_shape(int32_t n_chips, const int32_t *n_pix, const int32_t *n_obs, Shap
 // use, kept for the process's lifetime.
 std::mutex g_up_mu;
 hipStream_t g_up_stream[64] = {};
-hipStream_t shared_upload_stream(int device) {
+// (mask: when non-empty, the stream is created on those CUs -- the runtime may carry a copy out as
+// a blit kernel, which then runs on the reserved CUs instead of taking wave slots from detection)
+hipStream_t shared_upload_stream(int device, const std::vector<uint32_t> &mask) {
     if (device < 0 || device >= 64) return nullptr;
     std::lock_guard<std::mutex> g(g_up_mu);
-    if (!g_up_stream[device] && hipStreamCreateWithFlags(&g_up_stream[device], hipStreamNonBlocking) != hipSuccess)
-        g_up_stream[device] = nullptr;
+    if (!g_up_stream[device]) {
+        const hipError_t e = mask.empty() ? hipStreamCreateWithFlags(&g_up_stream[device], hipStreamNonBlocking)
+                                          : hipExtStreamCreateWithCUMask(&g_up_stream[device], (uint32_t)mask.size(), mask.data());
+        if (e != hipSuccess) g_up_stream[device] = nullptr;
+    }
     return g_up_stream[device];
 }
 
@@ -197,6 +202,7 @@ struct ccdgpu_ctx {
     const unsigned char *in_enc = nullptr;  // a transport-encoded batch the kernel reads in place
     // decode encoded uploads into the standard layout first (CCDGPU_DECODE=1: the round-3 path, A/B)
     bool decode_enc = false;
+    bool keep_slots = false;  // CCDGPU_KEEP_SLOTS=1 (measurement only): a slot stays staged after its run
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // the host waits for a detection through this event: blocking (the waiting thread sleeps on
     // the completion interrupt instead of polling), so the tile driver's waiting workers leave the
@@ -450,7 +456,9 @@ int ccdgpu_init_copy_cus(int device, int copy_cus, ccdgpu_ctx **out) {
     {
         const char *v = std::getenv("CCDGPU_SHARED_UPLOADS");
         if (!v || std::atoi(v) != 0) {
-            hipStream_t sh = shared_upload_stream(device);
+            const char *m = std::getenv("CCDGPU_UPLOAD_MASKED");
+            const bool um = masked && m && std::atoi(m) != 0;
+            hipStream_t sh = shared_upload_stream(device, um ? mask_copy : std::vector<uint32_t>());
             if (sh) c->up_stream = sh;
         }
     }
@@ -487,6 +495,7 @@ int ccdgpu_init_copy_cus(int device, int copy_cus, ccdgpu_ctx **out) {
     if (const char *v = std::getenv("CCDGPU_SLOTS_PER_CU")) c->slots_per_cu = std::max(1, std::atoi(v));
     if (const char *v = std::getenv("CCDGPU_POISON")) c->poison = std::atoi(v) != 0;
     if (const char *v = std::getenv("CCDGPU_DECODE")) c->decode_enc = std::atoi(v) != 0;
+    if (const char *v = std::getenv("CCDGPU_KEEP_SLOTS")) c->keep_slots = std::atoi(v) != 0;
     *out = c;
     return 0;
 }
@@ -814,7 +823,7 @@ static int slot_inputs(ccdgpu_ctx *c, int32_t slot) {
     c->in_qa = c->slot_encoded[slot] ? nullptr : c->slot_qa[slot].p;
     c->staged = true;
     c->ran = false;
-    c->slot_ready[slot] = false;
+    if (!c->keep_slots) c->slot_ready[slot] = false;
     return 0;
 }
 

@@ -47,35 +47,78 @@ encs = [ccdgpu.EncodedBatch.encode(chips, threads=8, drop_bits=drop, strict_bits
 cx = [0] * batch.n_chips
 
 
+KEPT = ('runenc', 'fetchenc', 'chain')  # slots staged once and kept (CCDGPU_KEEP_SLOTS=1): no uploads
+
+
 def trial(tag, n_ctx, copy_cus, mode='run'):
+    if mode in KEPT:
+        os.environ['CCDGPU_KEEP_SLOTS'] = '1'
     ctxs = [ccdgpu.Context(0, copy_cus=copy_cus) for _ in range(n_ctx)]
+    os.environ.pop('CCDGPU_KEEP_SLOTS', None)
     for c in ctxs:
         c.stage_chips(batch)
         c.run()
+        if mode in KEPT:
+            for s in range(3):
+                c.stage_slot_chips(s, encs[s])
     for c in ctxs:
         c.synchronize()
 
     def go(c):
         bufs = ccdgpu.RowsBuffers()
         for i in range(a.launches):
-            if mode == 'run':
+            if mode in ('run', 'noise'):
                 c.run()
             elif mode == 'fetch':
                 c.run()
                 c._keep = batch
                 c.fetch_batch_rows_into(cx, cx, bufs)
-            else:  # upload an encoded batch (pinned, prepared), detect, fetch rows
+            elif mode == 'runenc':  # encoded inputs read in place, no fetch
+                c.run_slot(i % 3)
+            elif mode == 'fetchenc':  # encoded inputs, detection then the separate rows fetch
+                c.run_slot(i % 3)
+                c.fetch_batch_rows_into(cx, cx, bufs)
+            elif mode == 'chain':  # encoded inputs, the batch chain, no uploads
+                c.run_slot_begin_rows(i % 3, cx, cx, bufs)
+                c.run_slot_end_rows()
+            elif mode == 'upload':  # upload an encoded batch (pinned, prepared), detect, fetch rows
                 c.stage_slot_chips(i % 3, encs[i % 3])
                 c.run_slot(i % 3)
                 c.fetch_batch_rows_into(cx, cx, bufs)
+            else:  # 'ahead': the runner's order -- the next upload staged while the detection runs
+                if i == 0:
+                    c.stage_slot_chips(0, encs[0])
+                c.run_slot_begin_rows(i % 3, cx, cx, bufs)
+                if i + 1 < a.launches:
+                    c.stage_slot_chips((i + 1) % 3, encs[(i + 1) % 3])
+                c.run_slot_end_rows()
 
     th = [threading.Thread(target=go, args=(c,)) for c in ctxs]
+    stop = threading.Event()
+    noise = None
+    if mode == 'noise':
+        # unrelated uploads at the tile's rate (one 8-chip encoded batch per ~28 ms) into a context
+        # that never detects: the DMA traffic without any launch depending on it
+        up = ccdgpu.Context(0, copy_cus=copy_cus)
+
+        def upload():
+            k = 0
+            while not stop.is_set():
+                up.stage_slot_chips(k % 3, encs[k % 3])
+                k += 1
+                time.sleep(0.028)
+        noise = threading.Thread(target=upload)
+        noise.start()
     t = time.perf_counter()
     for x in th:
         x.start()
     for x in th:
         x.join()
     el = time.perf_counter() - t
+    if noise is not None:
+        stop.set()
+        noise.join()
+        up.close()
     for c in ctxs:
         c.close()
     rate = n_ctx * a.launches * batch.total_pixels / el
