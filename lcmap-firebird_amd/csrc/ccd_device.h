@@ -113,6 +113,16 @@ int ccdk_scatter_dev(const ccdgpu_segment *pool, const int32_t *pool_seq, const 
                      const unsigned long long *overflow, int64_t cap, const int64_t *offsets,
                      const int64_t *chip_pix_off, int32_t n_chips, ccdgpu_segment *out, void *stream);
 int ccdk_row_counts(const int32_t *nseg, int64_t *offsets, int64_t n_pix, int64_t *rc, void *stream);
+// pool -> CSR (and, rows != nullptr, the float32 rows) in one pass; segment count from n_pool_dev
+// when given, else n_pool_host; writes nothing when *overflow (ccd_rows.hip)
+int ccdk_pool_rows(const ccdgpu_segment *pool, const int32_t *pool_seq, const unsigned long long *n_pool_dev,
+                   int64_t n_pool_host, const unsigned long long *overflow, int64_t cap, const int64_t *offsets,
+                   const int64_t *chip_pix_off, int32_t n_chips, ccdgpu_segment *out, const int64_t *row_off,
+                   const int32_t *chip_xy, int32_t width, ccdgpu_row *rows, int64_t rows_cap, int32_t blocks, void *stream);
+// pyccd.default's row for every pixel without a change model
+int ccdk_default_rows(const int32_t *nseg, int64_t n_pix, const unsigned long long *overflow,
+                      const int64_t *chip_pix_off, int32_t n_chips, const int64_t *row_off, const int32_t *chip_xy,
+                      int32_t width, ccdgpu_row *rows, int64_t rows_cap, void *stream);
 // pool -> CSR; the segment's pixel field becomes the pixel index within its chip
 int ccdk_scatter(const ccdgpu_segment *pool, const int32_t *pool_seq, int64_t n_pool,
                  const int64_t *offsets, const int64_t *chip_pix_off, int32_t n_chips, ccdgpu_segment *out,

@@ -202,6 +202,7 @@ struct ccdgpu_ctx {
     const unsigned char *in_enc = nullptr;  // a transport-encoded batch the kernel reads in place
     // decode encoded uploads into the standard layout first (CCDGPU_DECODE=1: the round-3 path, A/B)
     bool decode_enc = false;
+    bool rows_fused = true;   // CCDGPU_ROWS_FUSED=0 (A/B): the separate scatter and per-chip row packing
     bool keep_slots = false;  // CCDGPU_KEEP_SLOTS=1 (measurement only): a slot stays staged after its run
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // the host waits for a detection through this event: blocking (the waiting thread sleeps on
@@ -236,7 +237,7 @@ struct ccdgpu_ctx {
     // arguments, counters and statistics read back, CSR offsets): DMA from / to pinned memory,
     // where pageable memory would go through a runtime staging copy -- a blit kernel that has to
     // wait for free CUs while other contexts' detection kernels hold them all
-    PinBuf h_small, h_off, h_tab, h_fo;  // (h_tab: chip tables of a launch; h_fo: row-fetch offsets)
+    PinBuf h_small, h_off, h_tab, h_fo, h_xy;  // (h_tab: chip tables of a launch; h_fo: row-fetch offsets)
     DevBuf<int64_t> slot_dates[CCDGPU_UPLOAD_SLOTS];   // upload slots (ccdgpu_stage_slot / ccdgpu_run_slot)
     DevBuf<int16_t> slot_spectra[CCDGPU_UPLOAD_SLOTS];
     DevBuf<uint16_t> slot_qa[CCDGPU_UPLOAD_SLOTS];
@@ -297,6 +298,7 @@ struct ccdgpu_ctx {
         h_off.release();
         h_tab.release();
         h_fo.release();
+        h_xy.release();
         if (aux_own && aux) (void)hipStreamDestroy(aux);
         for (auto &e : ev)
             if (e) (void)hipEventDestroy(e);
@@ -412,10 +414,19 @@ int ccdgpu_init_copy_cus(int device, int copy_cus, ccdgpu_ctx **out) {
     // copy_cus = k > 0: the copy stream (uploads' decode kernel, blits) gets k CUs of its own --
     // the same k for every context -- and the detection stream the rest, so a context's upload is
     // never starved of CUs by other contexts' persistent detection waves (which otherwise hold
-    // every wave slot until their launch drains).  Reserved: the last ceil(k / 8) CUs of each
-    // group of n_cu / 8 (one group per XCD, if the mask numbers CUs XCD-major).  The environment
-    // variable CCDGPU_COPY_CUS overrides k (experiments).
+    // every wave slot until their launch drains).  The mask bits are the last ceil(k / 8) of each
+    // run of n_cu / 8.  The driver maps mask bit i to XCD i % 8 (the i / 8-th CU of that XCD,
+    // shader engines interleaved; tools/probe/cu_mask.hip, profiles/r04/cu_mask_probe.txt), so for
+    // k = 8 these are one shader engine of XCD 7: the detection stream runs on the other 248 CUs,
+    // and the copy / aux streams -- whose masks are empty on XCDs 0-6, which the hardware treats
+    // as unrestricted -- have those 8 CUs to themselves and share the rest.  The truly
+    // interleaved reservation (ceil(k / 8) CUs on every XCD and nothing else for the copy
+    // streams, CCDGPU_MASK_INTERLEAVED=1) measured slower: one context's detection 2.29M vs
+    // 2.44M px/s (the same as with no reservation), four contexts with the batch chain 2.62M vs
+    // 2.72M (profiles/r04/cu_layout_ab.txt).  CCDGPU_COPY_CUS overrides k (experiments).
     if (const char *e = std::getenv("CCDGPU_COPY_CUS")) copy_cus = std::max(0, std::atoi(e));
+    const char *mi = std::getenv("CCDGPU_MASK_INTERLEAVED");
+    const bool blocked = !(mi && std::atoi(mi) != 0);
     std::vector<uint32_t> mask_det, mask_copy;
     if (copy_cus > 0 && copy_cus < c->n_cu) {
         const int nw = (c->n_cu + 31) / 32, groups = 8, per = c->n_cu / groups;
@@ -430,9 +441,14 @@ int ccdgpu_init_copy_cus(int device, int copy_cus, ccdgpu_ctx **out) {
         mask_det.assign(nw, 0u);
         mask_copy.assign(nw, 0u);
         for (int cu = 0; cu < c->n_cu; ++cu) {
-            const bool reserved = (cu % per) >= per - k;
+            const bool reserved = blocked ? (cu % per) >= per - k : cu >= c->n_cu - groups * k;
             (reserved ? mask_copy : mask_det)[cu / 32] |= 1u << (cu % 32);
         }
+        // CCDGPU_AUX_WIDE=1 (A/B): the copy and aux streams may use every CU, the reserved ones
+        // being the CUs no detection wave can hold
+        if (const char *w = std::getenv("CCDGPU_AUX_WIDE"))
+            if (std::atoi(w) != 0)
+                for (int cu = 0; cu < c->n_cu; ++cu) mask_copy[cu / 32] |= 1u << (cu % 32);
     }
     const bool masked = !mask_det.empty();
     if ((masked ? hipExtStreamCreateWithCUMask(&c->stream, (uint32_t)mask_det.size(), mask_det.data())
@@ -495,6 +511,7 @@ int ccdgpu_init_copy_cus(int device, int copy_cus, ccdgpu_ctx **out) {
     if (const char *v = std::getenv("CCDGPU_SLOTS_PER_CU")) c->slots_per_cu = std::max(1, std::atoi(v));
     if (const char *v = std::getenv("CCDGPU_POISON")) c->poison = std::atoi(v) != 0;
     if (const char *v = std::getenv("CCDGPU_DECODE")) c->decode_enc = std::atoi(v) != 0;
+    if (const char *v = std::getenv("CCDGPU_ROWS_FUSED")) c->rows_fused = std::atoi(v) != 0;
     if (const char *v = std::getenv("CCDGPU_KEEP_SLOTS")) c->keep_slots = std::atoi(v) != 0;
     *out = c;
     return 0;
@@ -899,15 +916,33 @@ static int enqueue_rows(ccdgpu_ctx *c) {
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(c->cub_tmp.p, tmp_row, c->rowcnt.p, c->row_off.p, (int)np + 1, ax));
     // (on a pool overflow -- counters[3] -- the segment counts exceed what the pool holds: the scatter
     // and the row packing write nothing and ccdgpu_run_slot_end_rows reruns the batch)
-    if (ccdk_scatter_dev(c->pool.p, c->pool_seq.p, c->counters.p + 1, c->counters.p + 3, c->pool_cap, c->offsets.p,
-                         c->chip_pix_off.p, nc, c->csr.p, ax))
-        return fail(CCDGPU_EHIP, "scatter launch failed");
+    // the chips' (cx, cy) through pinned staging
+    if ((rc = c->row_xy.ensure(2 * (size_t)nc)) || (rc = c->h_xy.ensure(sizeof(int32_t) * 2 * (size_t)nc))) return rc;
+    int32_t *hxy = reinterpret_cast<int32_t *>(c->h_xy.p);
     for (int32_t ch = 0; ch < nc; ++ch) {
-        const int64_t q = sh.pix_off[ch];
-        if (ccdk_pack_rows(c->csr.p, c->offsets.p + q, c->row_off.p + q, c->mask.p + (size_t)q * c->mask_words,
-                           c->mask_words, sh.npix[ch], sh.nobs[ch], c->rq_cx[ch], c->rq_cy[ch], c->rq_width, c->rows.p,
-                           nullptr, c->counters.p + 3, c->pool_cap, rows_dev, ax))
+        hxy[2 * ch] = c->rq_cx[ch];
+        hxy[2 * ch + 1] = c->rq_cy[ch];
+    }
+    HIPCHK(hipMemcpyAsync(c->row_xy.p, hxy, sizeof(int32_t) * 2 * (size_t)nc, hipMemcpyHostToDevice, ax));
+    if (c->rows_fused) {
+        // pool -> CSR and rows in one pass, then the default rows of pixels without a model
+        if (ccdk_pool_rows(c->pool.p, c->pool_seq.p, c->counters.p + 1, 0, c->counters.p + 3, c->pool_cap, c->offsets.p,
+                           c->chip_pix_off.p, nc, c->csr.p, c->row_off.p, c->row_xy.p, c->rq_width, c->rows.p, rows_dev,
+                           256, ax) ||
+            ccdk_default_rows(c->nseg.p, np, c->counters.p + 3, c->chip_pix_off.p, nc, c->row_off.p, c->row_xy.p, c->rq_width,
+                              c->rows.p, rows_dev, ax))
             return fail(CCDGPU_EHIP, "row packing launch failed");
+    } else {
+        if (ccdk_scatter_dev(c->pool.p, c->pool_seq.p, c->counters.p + 1, c->counters.p + 3, c->pool_cap, c->offsets.p,
+                             c->chip_pix_off.p, nc, c->csr.p, ax))
+            return fail(CCDGPU_EHIP, "scatter launch failed");
+        for (int32_t ch = 0; ch < nc; ++ch) {
+            const int64_t q = sh.pix_off[ch];
+            if (ccdk_pack_rows(c->csr.p, c->offsets.p + q, c->row_off.p + q, c->mask.p + (size_t)q * c->mask_words,
+                               c->mask_words, sh.npix[ch], sh.nobs[ch], c->rq_cx[ch], c->rq_cy[ch], c->rq_width, c->rows.p,
+                               nullptr, c->counters.p + 3, c->pool_cap, rows_dev, ax))
+                return fail(CCDGPU_EHIP, "row packing launch failed");
+        }
     }
     const size_t ob = sizeof(int64_t) * (size_t)(np + 1);
     HIPCHK(hipMemcpyAsync(c->h_off.p, c->offsets.p, ob, hipMemcpyDeviceToHost, ax));
@@ -1148,7 +1183,9 @@ static int finish(ccdgpu_ctx *c, double *kernel_seconds, bool *again, bool chain
     HIPCHK(hipStreamSynchronize(ax));
     std::memcpy(c->h_offsets.data(), c->h_off.p, sizeof(int64_t) * (size_t)c->total_pix);
     c->h_offsets[c->total_pix] = c->n_pool;
-    if (ccdk_scatter(c->pool.p, c->pool_seq.p, c->n_pool, c->offsets.p, c->chip_pix_off.p, nc, c->csr.p, ax))
+    if (c->rows_fused ? ccdk_pool_rows(c->pool.p, c->pool_seq.p, nullptr, c->n_pool, nullptr, c->n_pool, c->offsets.p,
+                                       c->chip_pix_off.p, nc, c->csr.p, nullptr, nullptr, 1, nullptr, 0, 256, ax)
+                      : ccdk_scatter(c->pool.p, c->pool_seq.p, c->n_pool, c->offsets.p, c->chip_pix_off.p, nc, c->csr.p, ax))
         return fail(CCDGPU_EHIP, "scatter launch failed");
     HIPCHK(hipEventRecord(c->ev[3], ax));
     HIPCHK(hipStreamSynchronize(ax));

@@ -25,6 +25,7 @@ ap.add_argument('--config', type=int, default=3)
 ap.add_argument('--per', type=int, default=8)
 ap.add_argument('--launches', type=int, default=12)
 ap.add_argument('--modes', default='run,fetch,upload')
+ap.add_argument('--ns', default='1,4', help='context counts to run each mode with')
 ap.add_argument('--pool', action='store_true',
                 help="the bench tile leg's chips (TileSource pool mode: date-shifted copies of GPU-generated chips, "
                      "positions 0..per-1) instead of the resident leg's")
@@ -127,7 +128,7 @@ def trial(tag, n_ctx, copy_cus, mode='run'):
 
 
 for mode in a.modes.split(','):
-    for n in (1, 4):
+    for n in [int(x) for x in a.ns.split(',')]:
         trial('%s_n%d' % (mode, n), n, 8, mode)
 print(json.dumps({'per': a.per, 'launches': a.launches, 'pool': a.pool, 'rates': out,
                   'GPU_MAX_HW_QUEUES': os.environ.get('GPU_MAX_HW_QUEUES')}))
