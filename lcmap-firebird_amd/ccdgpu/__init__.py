@@ -589,11 +589,13 @@ class Context(object):
         n_pix = int(batch.pix_off[-1])
         words = (int(batch.n_obs.max()) + 31) // 32
         bufs.ensure(n_pix + 1, int(bufs.rows_per_pixel * n_pix) + 64, n_pix * words)
+        rate = bufs.copy_per_pixel if bufs.copy_per_pixel is not None else bufs.rows_per_pixel
+        cap = min(bufs.rows.size, int(rate * n_pix) + 64)
         _check(lib().ccdgpu_run_slot_begin_rows(self._ctx, int(slot), cx.ctypes.data, cy.ctypes.data, int(width),
                                                 bufs.offsets.ctypes.data, bufs.offsets.size, bufs.rows.ctypes.data,
-                                                bufs.rows.size, bufs.mask.ctypes.data, bufs.mask.size))
+                                                cap, bufs.mask.ctypes.data, bufs.mask.size))
         self._pending_slot = int(slot)
-        self._rows_req = (cx, cy, bufs, int(width), n_pix, words)
+        self._rows_req = (cx, cy, bufs, int(width), n_pix, words, cap)
 
     def run_slot_end_rows(self):
         """(row_offsets [n_pix+1], rows, mask words [n_pix][words]) of the batch begun with
@@ -602,13 +604,17 @@ class Context(object):
         secs = ctypes.c_double(0.0)
         nr = ctypes.c_int64(0)
         rc = lib().ccdgpu_run_slot_end_rows(self._ctx, ctypes.byref(secs), ctypes.byref(nr))
-        cx, cy, bufs, width, n_pix, words = self._rows_req
+        cx, cy, bufs, width, n_pix, words, cap = self._rows_req
         self._rows_req = None
         self._keep = self._slot_keep.get(self._pending_slot)
         self._n_pix = None
+        if nr.value > 0:
+            bufs.max_rate = max(bufs.max_rate, nr.value / max(1, n_pix))
+            bufs.copy_per_pixel = min(bufs.rows_per_pixel, 1.25 * bufs.max_rate)
         if rc == abi.E_OVERFLOW and nr.value > 0 and self._keep is not None and \
-                nr.value > bufs.rows.size and 'rows' in last_error():
+                nr.value > cap and 'rows' in last_error():
             bufs.rows_per_pixel = max(bufs.rows_per_pixel, 1.25 * nr.value / max(1, n_pix))
+            bufs.copy_per_pixel = min(bufs.rows_per_pixel, 1.25 * bufs.max_rate)
             self.qa_error = False
             return self.fetch_batch_rows_into(cx, cy, bufs, width)
         if rc not in (0, abi.E_QA):
@@ -738,6 +744,12 @@ class RowsBuffers(object):
     def __init__(self, pinned=True, rows_per_pixel=2.0):
         self.pinned = pinned
         self.rows_per_pixel = float(rows_per_pixel)  # rows room of a batch chain (run_slot_begin_rows)
+        # rows a batch chain copies back per pixel: learned from the batches seen (1.25 x the
+        # highest rate, at most rows_per_pixel), so the copy is not the whole room -- a tile of
+        # ~1 row per pixel copies ~1.25 instead of 2 rows' bytes per pixel; a batch with more
+        # rows than that takes the rows-overflow path once and raises the rate
+        self.copy_per_pixel = None
+        self.max_rate = 0.0
         self.offsets = np.zeros(0, np.int64)
         self.rows = np.zeros(0, abi.ROW_DTYPE)
         self.mask = np.zeros(0, np.uint32)

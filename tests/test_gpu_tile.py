@@ -166,6 +166,19 @@ def test_batch_chain_rows_equal_the_fetched_rows_and_overflow_falls_back():
             assert np.array_equal(got[2], ref[2]), rpp
             if rpp < 1:
                 assert bufs.rows_per_pixel > rpp  # learned from the overflow
+        # the copy size learned from a batch of ~1 row per pixel (C3 chips), then a batch with
+        # more rows per pixel than that: the overflow path, the same rows
+        bufs = ccdgpu.RowsBuffers()
+        enc3 = ccdgpu.EncodedBatch.encode(cs[1:], threads=4)
+        ctx.stage_slot_chips(2, enc3)
+        ctx.run_slot_begin_rows(2, cx[1:], cy[1:], bufs)
+        ctx.run_slot_end_rows()
+        assert bufs.copy_per_pixel is not None and bufs.copy_per_pixel < 2.0
+        ctx.stage_slot_chips(0, enc)
+        ctx.run_slot_begin_rows(0, cx, cy, bufs)
+        got = ctx.run_slot_end_rows()
+        assert got[1].tobytes() == ref[1].tobytes()
+        assert np.array_equal(got[0], ref[0]) and np.array_equal(got[2], ref[2])
     finally:
         ctx.close()
     assert ref[1].shape[0] > 900  # more rows than 0.5 per pixel
