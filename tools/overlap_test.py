@@ -26,6 +26,7 @@ ap.add_argument('--per', type=int, default=8)
 ap.add_argument('--launches', type=int, default=12)
 ap.add_argument('--modes', default='run,fetch,upload')
 ap.add_argument('--ns', default='1,4', help='context counts to run each mode with')
+ap.add_argument('--pool-offset', type=int, default=0, help='--pool: first tile position of the batch')
 ap.add_argument('--pool', action='store_true',
                 help="the bench tile leg's chips (TileSource pool mode: date-shifted copies of GPU-generated chips, "
                      "positions 0..per-1) instead of the resident leg's")
@@ -34,7 +35,7 @@ cfg = synth.config(a.config)
 if a.pool:
     src = synth.TileSource(cfg, device=0, batch_chips=a.per, mode='pool', pool_chips=32)
     src.prepare()
-    batch = ccdgpu.ChipBatch.from_chips([tuple(np.array(x) for x in v) for v in src.views(list(range(a.per)))])
+    batch = ccdgpu.ChipBatch.from_chips([tuple(np.array(x) for x in v) for v in src.views(list(range(a.pool_offset, a.pool_offset + a.per)))])
     src.close()
 else:
     ids = bench.chip_ids(0, 64, 1, lambda c: bench.synth_nobs(cfg, c))[::64 // a.per][:a.per]
@@ -130,5 +131,5 @@ def trial(tag, n_ctx, copy_cus, mode='run'):
 for mode in a.modes.split(','):
     for n in [int(x) for x in a.ns.split(',')]:
         trial('%s_n%d' % (mode, n), n, 8, mode)
-print(json.dumps({'per': a.per, 'launches': a.launches, 'pool': a.pool, 'rates': out,
+print(json.dumps({'per': a.per, 'launches': a.launches, 'pool': a.pool, 'pool_offset': a.pool_offset, 'rates': out,
                   'GPU_MAX_HW_QUEUES': os.environ.get('GPU_MAX_HW_QUEUES')}))
