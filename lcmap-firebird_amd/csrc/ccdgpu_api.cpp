@@ -203,7 +203,8 @@ struct ccdgpu_ctx {
     // decode encoded uploads into the standard layout first (CCDGPU_DECODE=1: the round-3 path, A/B)
     bool decode_enc = false;
     bool rows_fused = true;   // CCDGPU_ROWS_FUSED=0 (A/B): the separate scatter and per-chip row packing
-    bool keep_slots = false;  // CCDGPU_KEEP_SLOTS=1 (measurement only): a slot stays staged after its run
+    bool keep_slots = false;
+    int chain_skip = 0;       // CCDGPU_CHAIN_SKIP (measurement only): 1 no row / mask copies, 2 no CSR, 4 no row kernels  // CCDGPU_KEEP_SLOTS=1 (measurement only): a slot stays staged after its run
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // the host waits for a detection through this event: blocking (the waiting thread sleeps on
     // the completion interrupt instead of polling), so the tile driver's waiting workers leave the
@@ -512,6 +513,7 @@ int ccdgpu_init_copy_cus(int device, int copy_cus, ccdgpu_ctx **out) {
     if (const char *v = std::getenv("CCDGPU_POISON")) c->poison = std::atoi(v) != 0;
     if (const char *v = std::getenv("CCDGPU_DECODE")) c->decode_enc = std::atoi(v) != 0;
     if (const char *v = std::getenv("CCDGPU_ROWS_FUSED")) c->rows_fused = std::atoi(v) != 0;
+    if (const char *v = std::getenv("CCDGPU_CHAIN_SKIP")) c->chain_skip = std::atoi(v);
     if (const char *v = std::getenv("CCDGPU_KEEP_SLOTS")) c->keep_slots = std::atoi(v) != 0;
     *out = c;
     return 0;
@@ -924,11 +926,12 @@ static int enqueue_rows(ccdgpu_ctx *c) {
         hxy[2 * ch + 1] = c->rq_cy[ch];
     }
     HIPCHK(hipMemcpyAsync(c->row_xy.p, hxy, sizeof(int32_t) * 2 * (size_t)nc, hipMemcpyHostToDevice, ax));
-    if (c->rows_fused) {
+    if (c->chain_skip & 4) {
+    } else if (c->rows_fused) {
         // pool -> CSR and rows in one pass, then the default rows of pixels without a model
         if (ccdk_pool_rows(c->pool.p, c->pool_seq.p, c->counters.p + 1, 0, c->counters.p + 3, c->pool_cap, c->offsets.p,
-                           c->chip_pix_off.p, nc, c->csr.p, c->row_off.p, c->row_xy.p, c->rq_width, c->rows.p, rows_dev,
-                           256, ax) ||
+                           c->chip_pix_off.p, nc, (c->chain_skip & 2) ? nullptr : c->csr.p, c->row_off.p, c->row_xy.p,
+                           c->rq_width, c->rows.p, rows_dev, 256, ax) ||
             ccdk_default_rows(c->nseg.p, np, c->counters.p + 3, c->chip_pix_off.p, nc, c->row_off.p, c->row_xy.p, c->rq_width,
                               c->rows.p, rows_dev, ax))
             return fail(CCDGPU_EHIP, "row packing launch failed");
@@ -947,10 +950,10 @@ static int enqueue_rows(ccdgpu_ctx *c) {
     const size_t ob = sizeof(int64_t) * (size_t)(np + 1);
     HIPCHK(hipMemcpyAsync(c->h_off.p, c->offsets.p, ob, hipMemcpyDeviceToHost, ax));
     HIPCHK(hipMemcpyAsync(c->rq_offsets, c->row_off.p, ob, hipMemcpyDeviceToHost, ax));
-    const int64_t nrc = std::min<int64_t>(c->rq_rows_cap, rows_dev);
+    const int64_t nrc = (c->chain_skip & 1) ? 0 : std::min<int64_t>(c->rq_rows_cap, rows_dev);
     if (nrc > 0) HIPCHK(hipMemcpyAsync(c->rq_rows, c->rows.p, sizeof(ccdgpu_row) * (size_t)nrc, hipMemcpyDeviceToHost, ax));
     const size_t nbits = (size_t)np * c->mask_words;
-    if (nbits > 0) HIPCHK(hipMemcpyAsync(c->rq_mask, c->mask.p, sizeof(uint32_t) * nbits, hipMemcpyDeviceToHost, ax));
+    if (nbits > 0 && !(c->chain_skip & 1)) HIPCHK(hipMemcpyAsync(c->rq_mask, c->mask.p, sizeof(uint32_t) * nbits, hipMemcpyDeviceToHost, ax));
     HIPCHK(hipEventRecord(c->done_rows, ax));
     return 0;
 }
