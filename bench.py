@@ -74,7 +74,7 @@ def parse():
     ap.add_argument('--no-tile', action='store_true',
                     help='resident leg only (kernel A/B runs): value = the resident rate, not the headline metric')
     ap.add_argument('--tile-batch', type=int, default=8, help='chips per launch in the tile leg')
-    ap.add_argument('--tile-pool', type=int, default=32, help='generated chips behind the tile leg\'s chips (each position a date-shifted copy)')
+    ap.add_argument('--tile-pool', type=int, default=64, help='generated chips behind the tile leg\'s chips (each position a date-shifted copy; ~18 GB of host memory per rank; 32 / 64 / 128: the same rate, profiles/r04/tile_pool_ab.txt)')
     ap.add_argument('--tile-contexts', type=int, default=4, help='contexts per GPU in the tile leg')
     ap.add_argument('--tile-copy-cus', type=int, default=8, help='CUs each tile context reserves for its upload stream (ccdgpu_init_copy_cus; 0 = none)')
     ap.add_argument('--tile-copy-threads', type=int, default=3, help='host threads per batch encode (or pool-chip copy) in the tile leg source (4 contexts x 3 within the box\'s 16-CPU quota)')
