@@ -428,6 +428,10 @@ int ccdgpu_init_copy_cus(int device, int copy_cus, ccdgpu_ctx **out) {
     if (const char *e = std::getenv("CCDGPU_COPY_CUS")) copy_cus = std::max(0, std::atoi(e));
     const char *mi = std::getenv("CCDGPU_MASK_INTERLEAVED");
     const bool blocked = !(mi && std::atoi(mi) != 0);
+    // CCDGPU_MASK_FIRST=1 (A/B): the first bit of each run instead of the last (XCD 0's shader
+    // engine 0, where a one-workgroup copy kernel lands)
+    const char *mf = std::getenv("CCDGPU_MASK_FIRST");
+    const bool first = mf && std::atoi(mf) != 0;
     std::vector<uint32_t> mask_det, mask_copy;
     if (copy_cus > 0 && copy_cus < c->n_cu) {
         const int nw = (c->n_cu + 31) / 32, groups = 8, per = c->n_cu / groups;
@@ -442,7 +446,7 @@ int ccdgpu_init_copy_cus(int device, int copy_cus, ccdgpu_ctx **out) {
         mask_det.assign(nw, 0u);
         mask_copy.assign(nw, 0u);
         for (int cu = 0; cu < c->n_cu; ++cu) {
-            const bool reserved = blocked ? (cu % per) >= per - k : cu >= c->n_cu - groups * k;
+            const bool reserved = !blocked ? cu >= c->n_cu - groups * k : first ? (cu % per) < k : (cu % per) >= per - k;
             (reserved ? mask_copy : mask_det)[cu / 32] |= 1u << (cu % 32);
         }
         // CCDGPU_AUX_WIDE=1 (A/B): the copy and aux streams may use every CU, the reserved ones
