@@ -174,7 +174,7 @@ __global__ __launch_bounds__(256) void ccd_pool_rows(const ccdgpu_segment *__res
             const int64_t rd = __shfl(rdst, k);
             const int lpk = __shfl(lp, k);
             const uint32_t *src = reinterpret_cast<const uint32_t *>(pool + base + k);
-            if (d >= 0 && out) {
+            if (d >= 0 && out) {  // (out == nullptr: rows only)
                 uint32_t *dd = reinterpret_cast<uint32_t *>(out + d);
                 constexpr int PIXW = (int)(offsetof(ccdgpu_segment, pixel) / 4);
                 for (int i = l; i < SEG_DW; i += W) dd[i] = (i == PIXW) ? (uint32_t)lpk : src[i];

@@ -163,16 +163,11 @@ int make_shape(int32_t n_chips, const int32_t *n_pix, const int32_t *n_obs, Shap
 // use, kept for the process's lifetime.
 std::mutex g_up_mu;
 hipStream_t g_up_stream[64] = {};
-// (mask: when non-empty, the stream is created on those CUs -- the runtime may carry a copy out as
-// a blit kernel, which then runs on the reserved CUs instead of taking wave slots from detection)
-hipStream_t shared_upload_stream(int device, const std::vector<uint32_t> &mask) {
+hipStream_t shared_upload_stream(int device) {
     if (device < 0 || device >= 64) return nullptr;
     std::lock_guard<std::mutex> g(g_up_mu);
-    if (!g_up_stream[device]) {
-        const hipError_t e = mask.empty() ? hipStreamCreateWithFlags(&g_up_stream[device], hipStreamNonBlocking)
-                                          : hipExtStreamCreateWithCUMask(&g_up_stream[device], (uint32_t)mask.size(), mask.data());
-        if (e != hipSuccess) g_up_stream[device] = nullptr;
-    }
+    if (!g_up_stream[device] && hipStreamCreateWithFlags(&g_up_stream[device], hipStreamNonBlocking) != hipSuccess)
+        g_up_stream[device] = nullptr;
     return g_up_stream[device];
 }
 
@@ -203,8 +198,7 @@ struct ccdgpu_ctx {
     // decode encoded uploads into the standard layout first (CCDGPU_DECODE=1: the round-3 path, A/B)
     bool decode_enc = false;
     bool rows_fused = true;   // CCDGPU_ROWS_FUSED=0 (A/B): the separate scatter and per-chip row packing
-    bool keep_slots = false;
-    int chain_skip = 0;       // CCDGPU_CHAIN_SKIP (measurement only): 1 no row / mask copies, 2 no CSR, 4 no row kernels  // CCDGPU_KEEP_SLOTS=1 (measurement only): a slot stays staged after its run
+    bool keep_slots = false;  // CCDGPU_KEEP_SLOTS=1 (measurement only, tools/overlap_test.py): a slot stays staged after its run
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // the host waits for a detection through this event: blocking (the waiting thread sleeps on
     // the completion interrupt instead of polling), so the tile driver's waiting workers leave the
@@ -428,10 +422,6 @@ int ccdgpu_init_copy_cus(int device, int copy_cus, ccdgpu_ctx **out) {
     if (const char *e = std::getenv("CCDGPU_COPY_CUS")) copy_cus = std::max(0, std::atoi(e));
     const char *mi = std::getenv("CCDGPU_MASK_INTERLEAVED");
     const bool blocked = !(mi && std::atoi(mi) != 0);
-    // CCDGPU_MASK_FIRST=1 (A/B): the first bit of each run instead of the last (XCD 0's shader
-    // engine 0, where a one-workgroup copy kernel lands)
-    const char *mf = std::getenv("CCDGPU_MASK_FIRST");
-    const bool first = mf && std::atoi(mf) != 0;
     std::vector<uint32_t> mask_det, mask_copy;
     if (copy_cus > 0 && copy_cus < c->n_cu) {
         const int nw = (c->n_cu + 31) / 32, groups = 8, per = c->n_cu / groups;
@@ -446,14 +436,9 @@ int ccdgpu_init_copy_cus(int device, int copy_cus, ccdgpu_ctx **out) {
         mask_det.assign(nw, 0u);
         mask_copy.assign(nw, 0u);
         for (int cu = 0; cu < c->n_cu; ++cu) {
-            const bool reserved = !blocked ? cu >= c->n_cu - groups * k : first ? (cu % per) < k : (cu % per) >= per - k;
+            const bool reserved = blocked ? (cu % per) >= per - k : cu >= c->n_cu - groups * k;
             (reserved ? mask_copy : mask_det)[cu / 32] |= 1u << (cu % 32);
         }
-        // CCDGPU_AUX_WIDE=1 (A/B): the copy and aux streams may use every CU, the reserved ones
-        // being the CUs no detection wave can hold
-        if (const char *w = std::getenv("CCDGPU_AUX_WIDE"))
-            if (std::atoi(w) != 0)
-                for (int cu = 0; cu < c->n_cu; ++cu) mask_copy[cu / 32] |= 1u << (cu % 32);
     }
     const bool masked = !mask_det.empty();
     if ((masked ? hipExtStreamCreateWithCUMask(&c->stream, (uint32_t)mask_det.size(), mask_det.data())
@@ -477,9 +462,7 @@ int ccdgpu_init_copy_cus(int device, int copy_cus, ccdgpu_ctx **out) {
     {
         const char *v = std::getenv("CCDGPU_SHARED_UPLOADS");
         if (!v || std::atoi(v) != 0) {
-            const char *m = std::getenv("CCDGPU_UPLOAD_MASKED");
-            const bool um = masked && m && std::atoi(m) != 0;
-            hipStream_t sh = shared_upload_stream(device, um ? mask_copy : std::vector<uint32_t>());
+            hipStream_t sh = shared_upload_stream(device);
             if (sh) c->up_stream = sh;
         }
     }
@@ -517,7 +500,6 @@ int ccdgpu_init_copy_cus(int device, int copy_cus, ccdgpu_ctx **out) {
     if (const char *v = std::getenv("CCDGPU_POISON")) c->poison = std::atoi(v) != 0;
     if (const char *v = std::getenv("CCDGPU_DECODE")) c->decode_enc = std::atoi(v) != 0;
     if (const char *v = std::getenv("CCDGPU_ROWS_FUSED")) c->rows_fused = std::atoi(v) != 0;
-    if (const char *v = std::getenv("CCDGPU_CHAIN_SKIP")) c->chain_skip = std::atoi(v);
     if (const char *v = std::getenv("CCDGPU_KEEP_SLOTS")) c->keep_slots = std::atoi(v) != 0;
     *out = c;
     return 0;
@@ -930,11 +912,10 @@ static int enqueue_rows(ccdgpu_ctx *c) {
         hxy[2 * ch + 1] = c->rq_cy[ch];
     }
     HIPCHK(hipMemcpyAsync(c->row_xy.p, hxy, sizeof(int32_t) * 2 * (size_t)nc, hipMemcpyHostToDevice, ax));
-    if (c->chain_skip & 4) {
-    } else if (c->rows_fused) {
+    if (c->rows_fused) {
         // pool -> CSR and rows in one pass, then the default rows of pixels without a model
         if (ccdk_pool_rows(c->pool.p, c->pool_seq.p, c->counters.p + 1, 0, c->counters.p + 3, c->pool_cap, c->offsets.p,
-                           c->chip_pix_off.p, nc, (c->chain_skip & 2) ? nullptr : c->csr.p, c->row_off.p, c->row_xy.p,
+                           c->chip_pix_off.p, nc, c->csr.p, c->row_off.p, c->row_xy.p,
                            c->rq_width, c->rows.p, rows_dev, 256, ax) ||
             ccdk_default_rows(c->nseg.p, np, c->counters.p + 3, c->chip_pix_off.p, nc, c->row_off.p, c->row_xy.p, c->rq_width,
                               c->rows.p, rows_dev, ax))
@@ -954,10 +935,10 @@ static int enqueue_rows(ccdgpu_ctx *c) {
     const size_t ob = sizeof(int64_t) * (size_t)(np + 1);
     HIPCHK(hipMemcpyAsync(c->h_off.p, c->offsets.p, ob, hipMemcpyDeviceToHost, ax));
     HIPCHK(hipMemcpyAsync(c->rq_offsets, c->row_off.p, ob, hipMemcpyDeviceToHost, ax));
-    const int64_t nrc = (c->chain_skip & 1) ? 0 : std::min<int64_t>(c->rq_rows_cap, rows_dev);
+    const int64_t nrc = std::min<int64_t>(c->rq_rows_cap, rows_dev);
     if (nrc > 0) HIPCHK(hipMemcpyAsync(c->rq_rows, c->rows.p, sizeof(ccdgpu_row) * (size_t)nrc, hipMemcpyDeviceToHost, ax));
     const size_t nbits = (size_t)np * c->mask_words;
-    if (nbits > 0 && !(c->chain_skip & 1)) HIPCHK(hipMemcpyAsync(c->rq_mask, c->mask.p, sizeof(uint32_t) * nbits, hipMemcpyDeviceToHost, ax));
+    if (nbits > 0) HIPCHK(hipMemcpyAsync(c->rq_mask, c->mask.p, sizeof(uint32_t) * nbits, hipMemcpyDeviceToHost, ax));
     HIPCHK(hipEventRecord(c->done_rows, ax));
     return 0;
 }
