@@ -155,16 +155,22 @@ class ChainOracleContext(SplitOracleContext):
         n_pix = int(batch.pix_off[-1])
         words = (int(batch.n_obs.max()) + 31) // 32
         bufs.ensure(n_pix + 1, int(bufs.rows_per_pixel * n_pix) + 64, n_pix * words)
+        # the rows the chain copies back: the learned rate, as ccdgpu.Context does
+        rate = bufs.copy_per_pixel if bufs.copy_per_pixel is not None else bufs.rows_per_pixel
+        cap = min(bufs.rows.size, int(rate * n_pix) + 64)
         self.run_slot_begin(slot)
-        self._rows_req = (np.array(cx), np.array(cy), bufs, width)
+        self._rows_req = (np.array(cx), np.array(cy), bufs, width, n_pix, cap)
 
     def run_slot_end_rows(self):
         self.run_slot_end()
-        cx, cy, bufs, width = self._rows_req
+        cx, cy, bufs, width, n_pix, cap = self._rows_req
         self.chained += 1
-        cap = bufs.rows.size
         off, rows, bits = self.fetch_batch_rows(cx, cy, width)
+        if rows.size > 0:
+            bufs.max_rate = max(bufs.max_rate, rows.size / max(1, n_pix))
+            bufs.copy_per_pixel = min(bufs.rows_per_pixel, 1.25 * bufs.max_rate)
         if rows.size > cap:
             self.overflowed += 1
-            bufs.rows_per_pixel = max(bufs.rows_per_pixel, 1.25 * rows.size / max(1, off.size - 1))
+            bufs.rows_per_pixel = max(bufs.rows_per_pixel, 1.25 * rows.size / max(1, n_pix))
+            bufs.copy_per_pixel = min(bufs.rows_per_pixel, 1.25 * bufs.max_rate)
         return self.fetch_batch_rows_into(cx, cy, bufs, width)

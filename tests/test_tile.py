@@ -289,3 +289,41 @@ def test_tile_run_through_the_batch_chain_equals_the_plain_run():
                                  context_factory=lambda dev: OracleContext(dev, threads=2))
     assert [c['digest'] for c in res['chips']] == [c['digest'] for c in ref['chips']]
     assert sum(c.chained for c in made) == sum(st['batches'] for st in res['ranks'])
+
+
+def test_rows_copy_size_is_learned_and_an_overflow_still_returns_every_row():
+    """RowsBuffers' copy size of the batch chain: the rate learned from a batch (1.25 x rows per
+    pixel), not the whole room; a later batch with more rows per pixel than that takes the
+    overflow path and still returns every row (ChainOracleContext follows ccdgpu.Context)."""
+    import ccdgpu
+    from rows_util import ChainOracleContext
+    ctx = ChainOracleContext(0, threads=2, run_time=0.0)
+    bufs = ccdgpu.RowsBuffers(pinned=False)
+    from ccdgpu import synth
+    cfg = synth.config(3)
+    # 160 pixels a batch: more rows than the copy size's 64-row slack can hide
+    batches = [ccdgpu.ChipBatch.from_chips([synth.chip(cfg, p, 0, 160)]) for p in (0, 1)]
+    seen = []
+    for k, b in enumerate(batches):
+        ctx.stage_slot_chips(k % 2, b)
+        ctx.run_slot_begin_rows(k % 2, [0], [0], bufs)
+        off, rows, _ = ctx.run_slot_end_rows()
+        seen.append((np.array(off), rows.copy()))
+        assert bufs.copy_per_pixel is not None and bufs.copy_per_pixel <= bufs.rows_per_pixel
+    ref = []
+    for b in batches:
+        ctx.stage_slot_chips(0, b)
+        ctx.run_slot(0)
+        o, r, _ = ctx.fetch_batch_rows([0], [0])
+        ref.append((o, r))
+    for (o1, r1), (o2, r2) in zip(seen, ref):
+        assert np.array_equal(o1, o2) and r1.tobytes() == r2.tobytes()
+    # force a copy size below the next batch's rows: the overflow path, the same rows
+    bufs.copy_per_pixel = 0.01
+    bufs.max_rate = 0.0
+    before = ctx.overflowed
+    ctx.stage_slot_chips(0, batches[1])
+    ctx.run_slot_begin_rows(0, [0], [0], bufs)
+    off, rows, _ = ctx.run_slot_end_rows()
+    assert ctx.overflowed == before + 1
+    assert rows.tobytes() == ref[1][1].tobytes()
