@@ -234,8 +234,11 @@ int ccdgpu_run_slot_end(ccdgpu_ctx *ctx, double *kernel_seconds);
  * into the caller's buffers (pinned: ccdgpu_host_alloc), then returns; _end_rows waits once for
  * the whole chain and returns what ccdgpu_run_slot_end returns, with the row count in *n_rows.
  * More rows than rows_cap: CCDGPU_EOVERFLOW with *n_rows set -- the run is complete and
- * ccdgpu_fetch_batch_rows_into fetches its rows into larger buffers.  The buffers must stay
- * alive and untouched until _end_rows returns; ccdgpu_run_query works as for _begin. */
+ * ccdgpu_fetch_batch_rows_into fetches its rows into larger buffers.  rows_cap is also what the
+ * chain copies back (the whole rows_cap rows, written or not): pass the rows a batch is expected
+ * to hold, not the buffer's room (ccdgpu.RowsBuffers learns it: 1.25 x the highest rows per
+ * pixel seen).  The buffers must stay alive and untouched until _end_rows returns;
+ * ccdgpu_run_query works as for _begin. */
 int ccdgpu_run_slot_begin_rows(ccdgpu_ctx *ctx, int32_t slot, const int32_t *cx, const int32_t *cy, int32_t width,
                                int64_t *row_offsets, int64_t offsets_cap, ccdgpu_row *rows, int64_t rows_cap,
                                uint32_t *mask_bits, int64_t mask_cap);
