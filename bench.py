@@ -73,7 +73,7 @@ def parse():
                     help='tile leg only (knob sweeps): no resident leg, roofline null, no CPU baselines')
     ap.add_argument('--no-tile', action='store_true',
                     help='resident leg only (kernel A/B runs): value = the resident rate, not the headline metric')
-    ap.add_argument('--tile-batch', type=int, default=8, help='chips per launch in the tile leg')
+    ap.add_argument('--tile-batch', type=int, default=6, help='chips per launch in the tile leg (6: 2.71-2.72M px/s vs 2.68-2.70M with 8, profiles/r04/tile_batch_ab.txt)')
     ap.add_argument('--tile-pool', type=int, default=64, help='generated chips behind the tile leg\'s chips (each position a date-shifted copy; ~18 GB of host memory per rank; 32 / 64 / 128: the same rate, profiles/r04/tile_pool_ab.txt)')
     ap.add_argument('--tile-contexts', type=int, default=4, help='contexts per GPU in the tile leg')
     ap.add_argument('--tile-copy-cus', type=int, default=8, help='CUs each tile context reserves for its upload stream (ccdgpu_init_copy_cus; 0 = none)')

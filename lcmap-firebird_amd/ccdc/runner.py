@@ -457,7 +457,7 @@ def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, er
         ft.join()
 
 
-def detect_tile(xys, source, queue, device=0, contexts=4, batch_chips=8, params=None, width=100,
+def detect_tile(xys, source, queue, device=0, contexts=4, batch_chips=6, params=None, width=100,
                 sink=None, context_factory=None, upload_depth=2, tail_chips=None, bind_numa=True, encode=True,
                 encode_threads=3, copy_cus=8):
     """Change detection of the tile chips at ``xys`` (list of (cx, cy), tile order) on one GPU.
@@ -563,7 +563,7 @@ class TileError(RuntimeError):
         self.cause = cause
 
 
-def changedetection(tile, source, device=None, contexts=4, batch_chips=8, number=None, params=None,
+def changedetection(tile, source, device=None, contexts=4, batch_chips=6, number=None, params=None,
                     sink=None, width=100, context_factory=None, ctx=None, upload_depth=2, tail_chips=None,
                     bind_numa=True, encode=True, encode_threads=3, copy_cus=8):
     """Change detection for a tile on every GPU of the job (reference core.changedetection,

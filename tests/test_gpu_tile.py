@@ -113,7 +113,7 @@ def _full_inputs(pos, pixels):
 
 
 def test_full_size_tile_with_product_defaults_matches_oracle_on_stratified_pixels():
-    """ccdc.runner.changedetection as the tile leg runs it -- 4 contexts per GPU, 8-chip launches,
+    """ccdc.runner.changedetection as the tile leg runs it -- 4 contexts per GPU, 6-chip launches,
     8 CUs reserved per context for uploads, the 'unread' transport encoding, upload depth 2, split
     run with staging during detection -- over 24 distinct full-size (10^4-pixel) chips of both
     cadences with change-dense C5 chips mixed in (reference tile loop core.py:97-108 over
@@ -133,7 +133,7 @@ def test_full_size_tile_with_product_defaults_matches_oracle_on_stratified_pixel
     assert {c['n_obs'] for c in res['chips']} == {1421, 2121}
     assert all(c['n_pix'] == 10000 for c in res['chips'])
     st = res['ranks'][0]
-    assert st['batches'] <= 6, st  # (8-chip launches, not the tail's quarter batches throughout)
+    assert st['batches'] <= 8, st  # (full launches, not the tail's quarter batches throughout)
     out = tile_sample.check(sink, _full_inputs, threads=16)
     print('full-size tile parity: %s, runner %.1f s' % (out, run_s))
     assert out['pixels'] >= 100 * FULL_CHIPS - 5 and out['chips'] == FULL_CHIPS
