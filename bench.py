@@ -26,9 +26,9 @@ one ragged batch per step, K steps), the kernel behind the ``roofline`` (counted
 launch / the launch's duration vs the MI355X FP64 vector peak, 78.6 TFLOP/s: the path is FP64
 vector ALU, not a GEMM).  --config 2/4/5 selects the other synthetic configs for both legs.
 cpu_baseline = the C restatement oracle (oracle/libccdoracle.so, "port") on a bounded sample of
-the same chips on this host's cores (the box's 16-thread share of one GPU; the same on every
-affinity CPU as cpu_baseline_all_cores); cpu_baseline_pyccd_restatement = the pyccd-structured
-numpy restatement (oracle/ccd_ref.py) under multiprocessing.Pool on a fixed sample -- the
+the same chips on this host's cores (the box's 16-thread share of one GPU: the cgroup quota, so
+more threads only time-slice); cpu_baseline_pyccd_restatement = the pyccd-structured numpy
+restatement (oracle/ccd_ref.py), one worker process per core, on a fixed sample -- the
 stand-in for the reference's per-pixel ccd.detect (ccdc/pyccd.py:168), not installable here.
 """
 import argparse
@@ -289,8 +289,6 @@ def main():
             d, s, q = res['batch'].chip(0)
             out['cpu_baseline'] = cpu_baseline(res['batch'], args)
             out['speedup_vs_cpu_baseline'] = out['value'] / out['cpu_baseline']['value']
-            out['cpu_baseline_all_cores'] = cpu_baseline(res['batch'], args, all_cores=True)
-            out['speedup_vs_cpu_baseline_all_cores'] = out['value'] / out['cpu_baseline_all_cores']['value']
             out['cpu_baseline_pyccd_restatement'] = restatement_baseline(d, s, q, args)
             out['speedup_vs_pyccd_restatement'] = out['value'] / out['cpu_baseline_pyccd_restatement']['value']
         res.pop('batch')
@@ -372,15 +370,24 @@ def resident_leg(args, cfg, rank, world, device, dist, batch=None):
     achieved_tf = flops / (launch_ms * 1e-3) / 1e12
     mix = cadence_mix(batch)
     workload_key = 'config%d_chips%d_mix%s' % (args.config, len(ids), '-'.join('%dx%d' % (k, v) for k, v in sorted(mix.items())))
-    traffic = None
+    traffic, pmc_c = None, {}
     pmc_path = os.path.join(ROOT, 'profiles', 'pmc_detect.json')
     if os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))
             if pmc.get('workload') == workload_key:
                 traffic = pmc.get('hbm_bytes_per_launch')
+                pmc_c = pmc.get('counters', {})
         except Exception:
-            traffic = None
+            traffic, pmc_c = None, {}
+    # occupancy of the persistent launch: its resident wave slots over the SIMDs (4 per CU), and
+    # the same from the PMC pass (SQ_WAVES per launch); FP64 share of the VALU instructions
+    waves_per_simd = last.get('wave_slots', 0) / (4.0 * last['n_cu']) if last.get('n_cu') else None
+    f64 = sum(pmc_c.get(k, 0.0) for k in ('SQ_INSTS_VALU_ADD_F64', 'SQ_INSTS_VALU_FMA_F64', 'SQ_INSTS_VALU_MUL_F64',
+                                          'SQ_INSTS_VALU_TRANS_F64'))
+    fp64_share = f64 / pmc_c['SQ_INSTS_VALU'] if pmc_c.get('SQ_INSTS_VALU') else None
+    pmc_waves = pmc_c['SQ_WAVES'] / (4.0 * last['n_cu']) if pmc_c.get('SQ_WAVES') and last.get('n_cu') else None
+    wait_share = pmc_c.get('SQ_WAIT_ANY/SQ_WAVE_CYCLES')
     return {
         'value': value, 'unit': 'pixels/s', 'steps': args.steps, 'ms_per_step': elapsed / args.steps * 1e3,
         'workload': '%s; %d tile chips per GPU spread evenly over the tile (chip %d, %d, ..., %d; %s), one ragged batch '
@@ -411,6 +418,15 @@ def resident_leg(args, cfg, rank, world, device, dist, batch=None):
             'algorithmic_bytes_per_launch': alg_bytes,
             'algorithmic_hbm_gbs': alg_bytes / (launch_ms * 1e-3) / 1e9,
             'hbm_peak_gbs': HBM_PEAK_GBS,
+            'traffic_gbs': traffic / (launch_ms * 1e-3) / 1e9 if traffic else None,
+            'traffic_gbs_note': 'PMC HBM bytes per launch / kernel_ms_per_launch (L2-to-fabric traffic incl. '
+                                'Infinity-Cache hits, profiles/pmc_detect.json)',
+            'waves_per_simd': waves_per_simd,
+            'waves_per_simd_pmc': pmc_waves,
+            'waves_note': 'resident persistent waves / (4 SIMDs x CUs): launch configuration (ccdgpu_stats.wave_slots); '
+                          '_pmc = SQ_WAVES per launch of the PMC pass',
+            'fp64_share_of_valu': fp64_share,
+            'wait_share_of_wave_cycles': wait_share,
         },
         'segments_per_step': segs * world,
         'prep_ms_per_launch': float(np.mean(prep_ms)),
@@ -710,15 +726,13 @@ def host_cpus():
                  'omp_num_threads_share': share or None}
 
 
-def cpu_baseline(batch, args, all_cores=False):
+def cpu_baseline(batch, args):
     """C restatement oracle (oracle/libccdoracle.so) on a bounded pixel sample of the workload's
-    chips that share chip 0's date vector, OpenMP over pixels: on the box's CPU share of one GPU
-    (OMP_NUM_THREADS), or with ``all_cores`` on every CPU this process may run on."""
+    chips that share chip 0's date vector, OpenMP over pixels, on the box's CPU share of one GPU
+    (OMP_NUM_THREADS; the cgroup quota -- every affinity CPU would only time-slice on it)."""
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
     import oracle_ctypes
     thr, info = host_cpus()
-    if all_cores:
-        thr = info['affinity_cpus']
     dates = batch.chip(0)[0]
     same = [c for c in range(batch.n_chips) if np.array_equal(batch.chip(c)[0], dates)]
 
@@ -740,7 +754,7 @@ def cpu_baseline(batch, args, all_cores=False):
     t = time.perf_counter()
     oracle_ctypes.detect_batch(dates, S, Q, threads=thr)
     rate = n_probe / (time.perf_counter() - t)
-    secs = args.cpu_seconds if not all_cores else min(args.cpu_seconds, 5.0)
+    secs = args.cpu_seconds
     n = int(min(PIXELS_PER_CHIP * len(same), max(n_probe, rate * secs)))
     S, Q = sample(n)
     t = time.perf_counter()
@@ -748,53 +762,108 @@ def cpu_baseline(batch, args, all_cores=False):
     el = time.perf_counter() - t
     out = {'value': n / el, 'unit': 'pixels/s', 'cores': thr, 'kind': 'port',
            'sample': 'first %d pixels of the workload chips sharing chip 0\'s %d dates (%.1f s), C restatement oracle, '
-                     'OpenMP %d threads%s' % (n, dates.shape[0], el, thr, ' (every affinity CPU)' if all_cores else '')}
+                     'OpenMP %d threads' % (n, dates.shape[0], el, thr)}
     out.update(info)
     return out
 
 
-def _restatement_pixel(args):
-    import ccd_ref
-    d, s, q = args
-    return len(ccd_ref.detect(d, *[s[b] for b in range(7)], q)['change_models'])
+_RESTATEMENT_WORKER = r"""
+import sys, time
+import numpy as np
+sys.path[:0] = sys.argv[1:3]
+import ccd_ref
+z = np.load(sys.argv[3])
+d, S, Q = z['dates'], z['spectra'], z['qa']
+lo, hi = int(sys.argv[4]), int(sys.argv[5])
+ccd_ref.detect(d, *[S[b, lo] for b in range(7)], Q[lo])  # imports and first call outside the timing
+print('ready', flush=True)
+sys.stdin.readline()
+for p in range(lo, hi):
+    ccd_ref.detect(d, *[S[b, p] for b in range(7)], Q[p])
+print('done', flush=True)
+"""
 
 
 def restatement_baseline(dates, S, Q, args):
     """pyccd-equivalent restatement (oracle/ccd_ref.py: pyccd's module structure, numpy + a port
-    of scikit-learn 0.18's Lasso coordinate descent) under multiprocessing.Pool on a fixed
-    sample: the stand-in for reference pyccd's per-pixel ccd.detect at ccdc/pyccd.py:168 (pyccd
-    itself is not installable here)."""
-    import multiprocessing
-    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    of scikit-learn 0.18's Lasso coordinate descent) on a fixed sample, one worker process per
+    core of the box's share: the stand-in for reference pyccd's per-pixel ccd.detect at
+    ccdc/pyccd.py:168 run "via multiprocessing" (pyccd itself is not installable here, SURVEY.md
+    §8(c)).  Plain child processes (not a multiprocessing.Pool, whose resource tracker outlived
+    the bench as a stray process): each loads the sample, runs one untimed pixel, reports ready;
+    the timed region is from the common start signal to the last worker's end; every worker is
+    reaped before this returns."""
+    import subprocess
+    import tempfile
     thr, info = host_cpus()
     n = min(args.restatement_pixels, S.shape[1])
-    jobs = [(dates, S[:, p].copy(), Q[p].copy()) for p in range(n)]
-    ctx = multiprocessing.get_context('spawn')
-    pool = ctx.Pool(thr)
+    thr = max(1, min(thr, n))
+    fd, path = tempfile.mkstemp(suffix='.npz')
+    os.close(fd)
+    procs = []
     try:
-        pool.map(_restatement_pixel, jobs[:thr])  # worker start-up and imports outside the timing
+        np.savez(path, dates=dates, spectra=np.ascontiguousarray(S[:, :n]), qa=np.ascontiguousarray(Q[:n]))
+        cuts = [n * k // thr for k in range(thr + 1)]
+        env = dict(os.environ, OMP_NUM_THREADS='1', OPENBLAS_NUM_THREADS='1', MKL_NUM_THREADS='1')
+        for k in range(thr):
+            procs.append(subprocess.Popen(
+                [sys.executable, '-c', _RESTATEMENT_WORKER, os.path.join(ROOT, 'oracle'),
+                 os.path.join(ROOT, 'lcmap-firebird_amd'), path, str(cuts[k]), str(cuts[k + 1])],
+                stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env))
+        for pr in procs:
+            if pr.stdout.readline().strip() != 'ready':
+                raise RuntimeError('restatement worker failed to start')
         t = time.perf_counter()
-        pool.map(_restatement_pixel, jobs, chunksize=1)
+        for pr in procs:
+            pr.stdin.write('go\n')
+            pr.stdin.flush()
+        for pr in procs:
+            if pr.stdout.readline().strip() != 'done':
+                raise RuntimeError('restatement worker failed')
         el = time.perf_counter() - t
     finally:
-        pool.close()  # workers exit on their own (no terminate), then are reaped
-        pool.join()
+        for pr in procs:
+            if pr.poll() is None:
+                try:
+                    pr.stdin.close()
+                except OSError:
+                    pass
+            try:
+                pr.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                pr.kill()
+                pr.wait()
+        os.unlink(path)
     out = {'value': n / el, 'unit': 'pixels/s', 'cores': thr, 'kind': 'port',
            'label': 'pyccd-equivalent restatement (not pyccd itself)',
-           'sample': 'first %d pixels of chip 0 of the same workload (%d obs, %.1f s), oracle/ccd_ref.py, multiprocessing.Pool(%d)' % (
+           'sample': 'first %d pixels of chip 0 of the same workload (%d obs, %.1f s), oracle/ccd_ref.py, %d worker processes' % (
                n, dates.shape[0], el, thr)}
     out.update(info)
     return out
 
 
 def _stop_helpers():
-    """End the multiprocessing resource tracker the spawn pool started (it would otherwise
-    outlive the JSON line as a stray process)."""
+    """At exit: every process this bench started must be gone before the JSON line's run ends.
+    Lists any child still alive (to stderr, by pid and command line) and ends it."""
     try:
-        from multiprocessing import resource_tracker
-        resource_tracker._resource_tracker._stop()
-    except Exception:
-        pass
+        import psutil
+    except ImportError:
+        return
+    me = psutil.Process()
+    kids = me.children(recursive=True)
+    for k in kids:
+        try:
+            print('bench: ending leftover child process %d: %s' % (k.pid, ' '.join(k.cmdline())[:200]), file=sys.stderr)
+            k.terminate()
+        except psutil.Error:
+            pass
+    psutil.wait_procs(kids, timeout=5)
+    for k in kids:
+        try:
+            if k.is_running():
+                k.kill()
+        except psutil.Error:
+            pass
 
 
 if __name__ == '__main__':

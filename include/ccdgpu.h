@@ -319,6 +319,10 @@ typedef struct ccdgpu_stats {
     double detect_ms_device;    /* the detection kernel's execution window, first wave in to
                                    last wave out, on the device's 100 MHz clock (excludes time
                                    queued behind another context's launch)                 */
+    int64_t pool_reruns;        /* launches rerun because the segment pool overflowed      */
+    int64_t pool_cap;           /* segment-pool capacity after the run (segments)          */
+    int64_t wave_slots;         /* persistent detection waves of the launch (resident slots) */
+    int64_t n_cu;               /* compute units the detection kernel may use              */
 } ccdgpu_stats;
 int ccdgpu_last_stats(ccdgpu_ctx *ctx, ccdgpu_stats *stats);
 

@@ -611,11 +611,13 @@ class Context(object):
         if nr.value > 0:
             bufs.max_rate = max(bufs.max_rate, nr.value / max(1, n_pix))
             bufs.copy_per_pixel = min(bufs.rows_per_pixel, 1.25 * bufs.max_rate)
-        if rc == abi.E_OVERFLOW and nr.value > 0 and self._keep is not None and \
-                nr.value > cap and 'rows' in last_error():
+        short = (rc == abi.E_OVERFLOW and 'rows' in last_error()) or rc == abi.E_QA
+        if short and nr.value > cap and self._keep is not None:
+            # the run is complete but its rows did not fit: grow, learn the rate, fetch them (an
+            # unsupported QA value comes back as E_QA with the count set, and still raises)
             bufs.rows_per_pixel = max(bufs.rows_per_pixel, 1.25 * nr.value / max(1, n_pix))
             bufs.copy_per_pixel = min(bufs.rows_per_pixel, 1.25 * bufs.max_rate)
-            self.qa_error = False
+            self.qa_error = rc == abi.E_QA
             return self.fetch_batch_rows_into(cx, cy, bufs, width)
         if rc not in (0, abi.E_QA):
             _check(rc)

@@ -132,7 +132,8 @@ class Stats(ctypes.Structure):
     _fields_ = [('detect_ms', _f64), ('prep_ms', _f64), ('pixels', ctypes.c_int64),
                 ('segments', ctypes.c_int64), ('lasso_fits', ctypes.c_int64),
                 ('cd_sweeps', ctypes.c_int64), ('flops', ctypes.c_int64), ('bytes', ctypes.c_int64),
-                ('detect_ms_device', _f64)]
+                ('detect_ms_device', _f64), ('pool_reruns', ctypes.c_int64), ('pool_cap', ctypes.c_int64),
+                ('wave_slots', ctypes.c_int64), ('n_cu', ctypes.c_int64)]
 
 
 # parameter dict keys (pyccd parameters.yaml names) -> Params fields

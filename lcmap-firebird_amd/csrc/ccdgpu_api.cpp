@@ -210,6 +210,10 @@ struct ccdgpu_ctx {
     Shape shape;
     int32_t mask_words = 0, n_slots = 0;
     int64_t total_pix = 0, pool_cap = 0, n_pool = 0;
+    // initial segment-pool room per pixel (CCDGPU_POOL_PER_PIXEL, test knob: a small pool makes
+    // every change-dense batch take the overflow rerun) and the reruns of the last run
+    int pool_per_pixel = 8;
+    int64_t pool_reruns = 0;
     DevBuf<int64_t> dates, sdates, offsets;
     DevBuf<int16_t> spectra;
     DevBuf<uint16_t> qa;
@@ -501,6 +505,7 @@ int ccdgpu_init_copy_cus(int device, int copy_cus, ccdgpu_ctx **out) {
     if (const char *v = std::getenv("CCDGPU_DECODE")) c->decode_enc = std::atoi(v) != 0;
     if (const char *v = std::getenv("CCDGPU_ROWS_FUSED")) c->rows_fused = std::atoi(v) != 0;
     if (const char *v = std::getenv("CCDGPU_KEEP_SLOTS")) c->keep_slots = std::atoi(v) != 0;
+    if (const char *v = std::getenv("CCDGPU_POOL_PER_PIXEL")) c->pool_per_pixel = std::max(1, std::atoi(v));
     *out = c;
     return 0;
 }
@@ -574,7 +579,8 @@ static int stage_alloc(ccdgpu_ctx *c, const ccdgpu_params *params, const Shape &
     if ((rc = c->s_date.ensure(nper)) || (rc = c->s_row.ensure(nper * 8)) ||
         (rc = c->s_f64.ensure(ns * CCD_SLOT_F64(no))) || (rc = c->s_bk.ensure(ns * no)))
         return rc;
-    if (c->pool_cap < c->total_pix * 8) c->pool_cap = c->total_pix * 8;
+    if (c->pool_cap < c->total_pix * c->pool_per_pixel) c->pool_cap = c->total_pix * c->pool_per_pixel;
+    c->pool_reruns = 0;
     if ((rc = c->pool.ensure(c->pool_cap)) || (rc = c->pool_seq.ensure(c->pool_cap))) return rc;
     // chip tables, through the context's pinned staging (DMA, no runtime staging copy), on the
     // aux stream that runs the launch's prep; the previous launch's table copies are done
@@ -877,6 +883,18 @@ int ccdgpu_run_slot_end(ccdgpu_ctx *c, double *kernel_seconds) {
     return fail(CCDGPU_EOVERFLOW, "segment pool kept overflowing");
 }
 
+// An error after a detection was queued (the chain behind it could not be enqueued): wait for
+// everything the context queued, so no kernel still reads the slot or writes the pool when the
+// caller recovers and restages, then return the error.
+static int drain_after_error(ccdgpu_ctx *c, int rc) {
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->aux);
+    c->pending = false;
+    c->rows_mode = false;
+    c->pend_slot = -1;
+    return rc;
+}
+
 // The rest of a batch behind its detection, all on the aux stream (which already waits for the
 // detection's end): CSR offsets (scan), the closing entry and rows per pixel, row offsets
 // (scan), pool -> CSR with the device's segment count, row packing per chip, then the copies of
@@ -970,7 +988,8 @@ int ccdgpu_run_slot_begin_rows(ccdgpu_ctx *c, int32_t slot, const int32_t *cx, c
     c->rq_cx.assign(cx, cx + nc);
     c->rq_cy.assign(cy, cy + nc);
     detect_args(c, c->pend_args);
-    if ((rc = launch(c, c->pend_args)) || (rc = enqueue_rows(c))) return rc;
+    if ((rc = launch(c, c->pend_args))) return rc;
+    if ((rc = enqueue_rows(c))) return drain_after_error(c, rc);
     c->pending = true;
     c->rows_mode = true;
     c->pend_slot = slot;
@@ -993,13 +1012,17 @@ int ccdgpu_run_slot_end_rows(ccdgpu_ctx *c, double *kernel_seconds, int64_t *n_r
         if (!again) break;
         if (attempt == 3) return fail(CCDGPU_EOVERFLOW, "segment pool kept overflowing");
         int rc2;
-        if ((rc2 = launch(c, c->pend_args)) || (rc2 = enqueue_rows(c))) return rc2;
+        if ((rc2 = launch(c, c->pend_args))) return rc2;
+        if ((rc2 = enqueue_rows(c))) return drain_after_error(c, rc2);
     }
     if (rc && rc != CCDGPU_EQA) return rc;
     const int64_t nr = c->rq_offsets[c->total_pix];
     if (n_rows) *n_rows = nr;
     if (nr > c->rq_rows_cap) {
-        // the run is complete (ccdgpu_fetch_batch_rows_into fetches it into larger buffers)
+        // the run is complete (ccdgpu_fetch_batch_rows_into fetches it into larger buffers); an
+        // unsupported QA value outranks the short buffer -- CCDGPU_EQA with *n_rows set, so the
+        // caller both fetches every row and raises pyccd's ValueError
+        if (rc == CCDGPU_EQA) return rc;
         return fail(CCDGPU_EOVERFLOW, "run_slot_end_rows: " + std::to_string(nr) + " rows, the buffer holds " +
                                           std::to_string(c->rq_rows_cap));
     }
@@ -1141,6 +1164,7 @@ static int finish(ccdgpu_ctx *c, double *kernel_seconds, bool *again, bool chain
     if (h[4]) return fail(CCDGPU_EHIP, "kernel index guard tripped at ccd_kernels.hip line " + std::to_string(h[4]));
     if (h[3]) {  // pool overflow: grow and rerun
         c->pool_cap = (int64_t)(h[1] + h[1] / 4 + 1024);
+        ++c->pool_reruns;
         int rc;
         if ((rc = c->pool.ensure(c->pool_cap)) || (rc = c->pool_seq.ensure(c->pool_cap))) return rc;
         *again = true;
@@ -1186,6 +1210,10 @@ static int finish(ccdgpu_ctx *c, double *kernel_seconds, bool *again, bool chain
     c->last.lasso_fits = (int64_t)st[0];
     c->last.cd_sweeps = (int64_t)st[1];
     c->last.flops = (int64_t)st[2];
+    c->last.pool_reruns = c->pool_reruns;
+    c->last.pool_cap = c->pool_cap;
+    c->last.wave_slots = c->n_slots;
+    c->last.n_cu = c->n_cu;
     const int64_t in_bytes = sh.total_data() * 16 + sh.total_obs() * 8;
     const int64_t out_bytes = c->n_pool * (int64_t)sizeof(ccdgpu_segment) + c->total_pix * ((int64_t)c->mask_words * 4 + 4 + 24 + 4);
     c->last.bytes = in_bytes + out_bytes;

@@ -61,6 +61,28 @@ def synth_case(which, chip, n_pix, **over):
     return synth.chip(cfg, chip, 0, n_pix)
 
 
+REF_ARD12 = {  # values of the docstring example at reference ccdc/timeseries.py:105-115 (data)
+    'blues': [-9999, 295, -9999, 204, -9999, 238, -9999, -9999, 195, -9999, -9999, -9999],
+    'greens': [-9999, 499, -9999, 422, -9999, 363, -9999, -9999, 334, -9999, -9999, -9999],
+    'reds': [-9999, 413, -9999, 324, -9999, 315, -9999, -9999, 264, -9999, -9999, -9999],
+    'nirs': [-9999, 2329, -9999, 2379, -9999, 2115, -9999, -9999, 1629, -9999, -9999, -9999],
+    'swir1s': [-9999, 1322, -9999, 1205, -9999, 1100, -9999, -9999, 743, -9999, -9999, -9999],
+    'swir2s': [-9999, 593, -9999, 593, -9999, 522, -9999, -9999, 375, -9999, -9999, -9999],
+    'thermals': [-9999, 3020, -9999, 2930, -9999, 2902, -9999, -9999, 2920, -9999, -9999, -9999],
+    'qas': [1, 66, 1, 322, 1, 66, 1, 1, 66, 1, 1, 1],
+    'dates': [734992, 734991, 734984, 734983, 734976, 734975, 734448, 734441, 734439, 727265, 726648, 726616],
+}
+BAND_KEYS = ('blues', 'greens', 'reds', 'nirs', 'swir1s', 'swir2s', 'thermals')
+
+
+def ref_ard12():
+    r = REF_ARD12
+    d = np.array(r['dates'], dtype=np.int64)
+    s = np.array([r[k] for k in BAND_KEYS], dtype=np.int16)[:, None, :]
+    q = np.array(r['qas'], dtype=np.uint16)[None, :]
+    return d, s, q
+
+
 def edge_cases():
     """Hand-built inputs exercising the branches the reference's tests and pyccd's procedures
     name: the reference's all-fill element, few observations, insufficient clear, permanent
@@ -69,6 +91,10 @@ def edge_cases():
     # reference test/__init__.py:37-46 timeseries_element (4 obs, qa = 1 fill)
     d = np.array([734973, 731205, 724404, 723868], dtype=np.int64)
     cases['ref_fill4'] = (d, np.full((7, 1, 4), -9999, dtype=np.int16), np.ones((1, 4), dtype=np.uint16))
+    # reference ccdc/timeseries.py:105-115: the one merlin ARD record the reference holds (12 obs,
+    # dates descending as merlin emits them, -9999 fill, qas 1 / 66 / 322); band order blue,
+    # green, red, nir, swir1, swir2, thermal
+    cases['ref_ard12'] = ref_ard12()
     base_d, base_s, base_q = synth_case(2, 5, 8)
     n = base_d.shape[0]
     order = np.argsort(base_d)

@@ -68,3 +68,48 @@ def test_init_rejects_a_negative_cu_reservation():
 def test_header_constants_match_the_binding():
     txt = open(os.path.join(ROOT, 'include', 'ccdgpu.h')).read()
     assert int(re.search(r'#define CCDGPU_UPLOAD_SLOTS (\d+)', txt).group(1)) == ccdgpu.UPLOAD_SLOTS
+
+
+def test_stats_struct_carries_the_pool_fields():
+    names = [n for n, _ in abi.Stats._fields_]
+    assert names[-4:] == ['pool_reruns', 'pool_cap', 'wave_slots', 'n_cu']
+    txt = open(os.path.join(ROOT, 'include', 'ccdgpu.h')).read()
+    body = txt[txt.index('typedef struct ccdgpu_stats'):txt.index('} ccdgpu_stats;')]
+    assert re.findall(r'\b(\w+);', body) == names
+
+
+class _FakeLib(object):
+    """ccdgpu_run_slot_end_rows of a finished batch: return code ``rc``, ``rows`` rows"""
+
+    def __init__(self, rc, rows, msg):
+        self.rc, self.rows, self.msg = rc, rows, msg
+
+    def ccdgpu_run_slot_end_rows(self, ctx, secs, nr):
+        nr._obj.value = self.rows
+        return self.rc
+
+    def ccdgpu_last_error(self):
+        return self.msg.encode()
+
+
+@pytest.mark.parametrize('rc,msg,qa', [(abi.E_QA, 'unsupported bit-packed QA value (pixel 7)', True),
+                                       (abi.E_OVERFLOW, 'run_slot_end_rows: 900 rows, the buffer holds 264', False)])
+def test_run_slot_end_rows_fetches_short_rows_and_keeps_the_qa_error(monkeypatch, rc, msg, qa):
+    """Context.run_slot_end_rows (ccdgpu/__init__.py) after a chain whose rows did not fit the copy:
+    the rows are fetched into grown buffers whether the library says CCDGPU_EOVERFLOW or -- the
+    batch also holding an unsupported QA value -- CCDGPU_EQA with the row count set; qa_error
+    follows the return code (the tile runner raises on it)."""
+    ctx = object.__new__(ccdgpu.Context)
+    ctx.qa_error = False
+    ctx._ctx = None
+    bufs = ccdgpu.RowsBuffers(pinned=False, rows_per_pixel=0.5)
+    ctx._rows_req = ([0], [0], bufs, 100, 400, 13, 264)
+    ctx._pending_slot = 0
+    ctx._slot_keep = {0: object()}
+    fetched = []
+    ctx.fetch_batch_rows_into = lambda cx, cy, b, w: fetched.append(b) or ('rows',)
+    monkeypatch.setattr(ccdgpu, 'lib', lambda: _FakeLib(rc, 900, msg))
+    out = ctx.run_slot_end_rows()
+    assert out == ('rows',) and fetched == [bufs]
+    assert ctx.qa_error is qa
+    assert bufs.rows_per_pixel >= 1.25 * 900 / 400

@@ -240,3 +240,49 @@ def test_cu_reservation_extremes_keep_both_stream_masks_nonempty():
             ctx.close()
         assert g.segments.tobytes() == r.segments.tobytes(), cus
         assert np.array_equal(g.mask, r.mask), cus
+
+
+def test_reference_ard_record_through_hip_path():
+    """The one multi-date ARD record the reference holds (ccdc/timeseries.py:105-115: merlin's
+    layout -- 12 observations, dates descending, -9999 fill, qas 1 / 66 / 322) through
+    ccdc.pyccd.detect (pyccd.py:151-168) and ccd.detect on the GPU: the same procedure, processing
+    mask (sorted-date order), models and probabilities as the C oracle and the numpy restatement
+    (golden ref_ard12); pyccd.format's row carries the input-order ISO dates and the sorted mask."""
+    import datetime
+    import ccd
+    import ccd_ref
+    from ccdc import pyccd
+    sys_path_golden()
+    import make_golden
+    rec = dict((k, np.array(v, dtype=np.uint16 if k == 'qas' else np.int16)) for k, v in make_golden.REF_ARD12.items()
+               if k != 'dates')
+    rec['dates'] = list(make_golden.REF_ARD12['dates'])
+    (d, s, q), params, gold = golden_util.load('ref_ard12')
+    r = ccd.detect(**rec)
+    cpu = ccd_ref.detect(np.array(rec['dates']), *[rec[k] for k in make_golden.BAND_KEYS], rec['qas'])
+    rc, orc = oracle_ctypes.detect_batch(d, s, q, threads=1)
+    assert rc == 0
+    assert r['procedure'] == cpu['procedure'] == abi.PROCEDURES[int(orc.procedure[0])] == 'standard_procedure'
+    assert list(map(int, r['processing_mask'])) == list(map(int, cpu['processing_mask'])) == \
+        list(orc.mask[0].astype(int)) == list(gold.mask[0].astype(int))
+    assert r['change_models'] == cpu['change_models'] == []
+    for k in ('cloud_prob', 'snow_prob', 'water_prob'):
+        assert r[k] == pytest.approx(cpu[k], rel=1e-12)
+    # 4 clear of 12 (fill otherwise): too few for a model window -> pyccd.default's row
+    assert sum(r['processing_mask']) == 4
+    rows = pyccd.detect(((-1815585, 1064805, -1815585, 1064805), rec))
+    assert len(rows) == 1
+    row = rows[0]
+    assert row['sday'] == row['eday'] == row['bday'] == '0001-01-01'
+    assert row['dates'] == [datetime.date.fromordinal(x).isoformat() for x in rec['dates']]
+    srt = np.argsort(np.array(rec['dates']), kind='stable')
+    assert row['mask'] == [int(rec['qas'][i] in (66, 322)) for i in srt]
+    assert list(map(int, row['mask'])) == list(gold.mask[0].astype(int))
+
+
+def sys_path_golden():
+    import os
+    import sys
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+    if p not in sys.path:
+        sys.path.insert(0, p)

@@ -24,7 +24,7 @@ def test_c_oracle_matches_golden(name):
 
 
 def test_numpy_restatement_reproduces_golden_edges():
-    for name in ('ref_fill4', 'mixed_edge'):
+    for name in ('ref_fill4', 'ref_ard12', 'mixed_edge'):
         (d, s, q), params, ref = golden_util.load(name)
         for px in range(q.shape[0]):
             r = ccd_ref.detect(d, *[s[b, px] for b in range(7)], q[px], params=params)
