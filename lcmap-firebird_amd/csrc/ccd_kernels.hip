@@ -58,8 +58,16 @@ struct __attribute__((aligned(16))) Lds {
         double row[TR][RW];       // staging tile (Gram, Tmask, speculative fits, variogram counts)
         double ring[NB * PSTR];   // peek residuals, band-major [band][PSTR] (never live with a tile)
     };
-    double G[8][8];
-    double Q[8][8];  // Q[j][band] = Xc_j . yc_band
+    union {
+        struct {
+            double G[8][8];
+            double Q[8][8];  // Q[j][band] = Xc_j . yc_band
+        };
+        // lookforward between two fits (G / Q are rebuilt at every fit): per block of 46 bins of
+        // u = 4 t mod 1461, the fit window's squared residuals of the current models summed per
+        // band in float, every term rounded up (fit_bounds)
+        float blk[32][8];
+    };
     double YY[8];
     double xm[8];
     double ym[8];
@@ -2402,6 +2410,283 @@ __device__ __forceinline__ void build_closest(const Px &P, int fa, int fb, int k
     gsync();
 }
 
+// 16-byte bucket records in the slot's global scratch (a native vector type: loads and stores
+// through the address_space(1) pointer are single dwordx4 instructions)
+typedef unsigned rec4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void rec_store(GLOBAL_AS double *fs, int pos, uint4 q) {
+    reinterpret_cast<GLOBAL_AS rec4 *>(fs)[pos] = rec4{q.x, q.y, q.z, q.w};
+}
+__device__ __forceinline__ uint4 rec_load(const GLOBAL_AS double *fs, int pos) {
+    const rec4 v = reinterpret_cast<const GLOBAL_AS rec4 *>(fs)[pos];
+    return uint4{v.x, v.y, v.z, v.w};
+}
+
+// L->hist2 (bin counts of build_hist) -> bin start positions (ends = false: the cursors of a
+// counting-sort fill, which leaves the ends) or bin end positions (ends = true).  Lane l owns
+// words [12 l, 12 l + 12) (24 bins; 732 = 61 lanes x 12).
+__device__ __forceinline__ void bins_prefix(bool ends) {
+    Lds *L = &LDS();
+    const int l = lane();
+    unsigned hv[12];
+    const bool hl = l < 61;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) hv[i] = hl ? L->hist2[12 * l + i] : 0u;
+    int tot = 0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) tot += (int)(hv[i] & 0xFFFFu) + (int)(hv[i] >> 16);
+    int run = wscan_incl(tot) - tot;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+        const int s0 = run;
+        const int s1 = run + (int)(hv[i] & 0xFFFFu);
+        run = s1 + (int)(hv[i] >> 16);
+        if (hl) L->hist2[12 * l + i] = ends ? ((unsigned)s1 | ((unsigned)run << 16)) : ((unsigned)s0 | ((unsigned)s1 << 16));
+    }
+    wsync();
+}
+
+// Counting sort of the fit window [fa, fb) by u = 4 t mod 1461 (L->hist2: bin end positions
+// afterwards) into bucket records: P.fs viewed as 16-byte rows, record pos = the period row (7
+// band values + sorted index) of the pos-th entry in bucket order.  The records depend on the fit
+// window's rows only, not on the model: a step that needs its comparison rmse recomputes the
+// residuals of its 24 entries from them (coop_comp), so a refit writes 16 B per fit observation
+// instead of the squared residuals of every detection band (40 B) and computes no residuals --
+// and only when some step of its batches needs the exact comparison rmse.  Removals after the
+// window (lookforward outliers) leave the window's rows as they are.
+__device__ __forceinline__ void build_buckets(const Px &P, int fa, int fb) {
+    Lds *L = &LDS();
+    const int l = lane();
+    const int nf = fb - fa;
+    build_hist(P, fa, fb);
+    bins_prefix(false);
+    // four chunks per round: the row and date loads go out together, then the bin cursors
+    constexpr int U = 4;
+    for (int i0 = fa; i0 < fb; i0 += U * W) {
+        uint4 q[U];
+        int dt[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * W + l;
+            q[u] = uint4{0u, 0u, 0u, 0u};
+            dt[u] = 0;
+            if (i < fb) {
+                q[u] = CROW4(P, i);
+                dt[u] = CDR(P, i);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * W + l;
+            if (i < fb) {
+                const int ub = u1461(dt[u]);
+                const unsigned old = atomicAdd(&L->hist2[ub >> 1], 1u << ((ub & 1) * 16));
+                rec_store(P.fs, gidx(P, (int)((old >> ((ub & 1) * 16)) & 0xFFFFu), nf, __LINE__), q[u]);
+            }
+        }
+    }
+    gsync();  // the records are read by other lanes
+}
+
+// Per fit (lookforward, more than 24 fit observations), once it is needed: lasso.fitted_model's
+// rmse of the current models over the fit window [fa, fb) -- the same arithmetic, per-lane order
+// and wave reduction as build_closest's (lane l sums observations fa + l, fa + l + 64, ...), so
+// the value is bit-identical to it -- and, from the same residuals, the comparison-rmse bounds of
+// the batched steps: the window's bin end positions (L->hist2) and per block of 46 bins the sum
+// of its squared residuals per detection band (L->blk, float, every term rounded up).
+__device__ __forceinline__ void fit_bounds(const Px &P, int fa, int fb, int k) {
+    Lds *L = &LDS();
+    const int l = lane();
+    const int nf = fb - fa;
+    const unsigned dm = det_mask();
+    build_hist(P, fa, fb);
+    bins_prefix(true);
+    float *bz = &L->blk[0][0];
+    for (int i = l; i < 32 * 8; i += W) bz[i] = 0.0f;
+    wsync();
+    double ssq[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) ssq[b] = 0.0;
+    // two chunks per round, software-pipelined as build_closest: the next round's rows and dates
+    // load while this round's design rows load (lane l still adds fa + l, fa + l + 64, ... in order)
+    uint4 qn[2];
+    int dn[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int i = fa + u * W + l;
+        qn[u] = uint4{0u, 0u, 0u, 0u};
+        dn[u] = 0;
+        if (i < fb) {
+            qn[u] = CROW4(P, i);
+            dn[u] = CDR(P, i);
+        }
+    }
+    for (int i0 = fa; i0 < fb; i0 += 2 * W) {
+        uint4 qv[2];
+        int dt[2];
+        double xv[2][7];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            qv[u] = qn[u];
+            dt[u] = dn[u];
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int i = i0 + u * W + l;
+            const GLOBAL_AS double *bs = P.basis + (size_t)gidx(P, i < fb ? (int)(qv[u].w >> 16) : 0, P.n, __LINE__) * CCD_BASIS_STRIDE;
+#pragma unroll
+            for (int c = 0; c < 7; ++c) xv[u][c] = bs[c];
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int i = i0 + (2 + u) * W + l;
+            qn[u] = uint4{0u, 0u, 0u, 0u};
+            dn[u] = 0;
+            if (i < fb) {
+                qn[u] = CROW4(P, i);
+                dn[u] = CDR(P, i);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int i = i0 + u * W + l;
+            if (i >= fb) continue;
+            const int blk = u1461(dt[u]) / 46;
+            const double *x = xv[u];
+            const unsigned qw[4] = {qv[u].x, qv[u].y, qv[u].z, qv[u].w};
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                const double *c = L->coef[b];
+                double pr = x[0] * c[0];
+#pragma unroll
+                for (int jj = 1; jj < 7; ++jj) pr += x[jj] * c[jj];
+                pr += c[7];
+                const double y = (double)(int16_t)(qw[b >> 1] >> ((b & 1) * 16));
+                const double r = y - pr;
+                ssq[b] += r * r;
+                if ((dm >> b) & 1u) {
+                // r^2 rounded up to float without a rounding-mode switch: the nearest float, one
+                // ulp up when below (r^2 >= 0; NaN / inf pass through)
+                const double r2 = r * r;
+                float f = (float)r2;
+                f = (double)f < r2 ? __int_as_float(__float_as_int(f) + 1) : f;
+                atomicAdd(&L->blk[blk][b], f);
+            }
+            }
+        }
+    }
+    const double den = (double)(nf - (ARGS().p.rmse_dof ? k : 0));
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const double t = wsum(ssq[b]);
+        if (l == b) L->rmse[b] = sqrt(t / den);
+    }
+    wsync();
+}
+
+// find_closest_doy comparison rmse of ONE batched step (reference date dref) from the bucket
+// records, the whole wave working on it: the distance K of the 24th closest entry by a scan over
+// the bin ends (as closest_doy_scan), then lane = entry -- the circular run of bucket positions
+// closer than K and the entries at exactly K (the lowest sorted indices of those taken: the
+// stable argsort's tie rule; sorted index order is fit-window order) -- each taken lane
+// recomputes its residuals of the detection bands from its record and design row (resid_at's
+// arithmetic) and the squares are summed over the wave.  Returns sqrt(sum) / 4 of the s-th
+// detection band in out[s] (every lane).  nf > 24.
+__device__ __forceinline__ void coop_comp(const Px &P, int nf, int dref, const int (&bs)[NB], int nd,
+                                          double (&out)[NB]) {
+    const unsigned dm = det_mask();
+    const Lds *L = &LDS();
+    const int l = lane();
+    const int u = u1461(dref);
+    int K = 0, less = 0;
+    {
+        int carry = 0;
+        for (int base = 0; base <= 730; base += W) {
+            const int dd = base + l;
+            int c = 0;
+            if (dd == 0) c = bcount(L, u);
+            else if (dd <= 730) c = bcount(L, (u + dd) % 1461) + bcount(L, (u - dd + 1461) % 1461);
+            const int cum = wscan_incl(c) + carry;
+            const unsigned long long hit = bal(cum >= 24);
+            if (hit) {
+                const int src = __ffsll((long long)hit) - 1;
+                K = base + src;
+                less = rdl(cum, src) - rdl(c, src);
+                break;
+            }
+            carry = rdl(cum, W - 1);
+        }
+    }
+    const int need = 24 - less;
+    const int s0 = K > 0 ? bstart(L, (u - K + 1 + 1461) % 1461) : 0;
+    const int b1 = (u - K + 1461) % 1461, b2 = (u + K) % 1461;
+    const int c1 = bcount(L, b1), c2 = K > 0 ? bcount(L, b2) : 0;
+    const int st1 = bstart(L, b1), st2 = bstart(L, b2);
+    const int T = c1 + c2, E = less + T;
+    double acc[NB];  // per band (detection bands only)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[b] = 0.0;
+    for (int e0 = 0; e0 < E; e0 += W) {
+        const int e = e0 + l;
+        const bool tie = e >= less && e < E;
+        int pos = 0;
+        if (e < less) {
+            pos = s0 + e;
+            pos = pos >= nf ? pos - nf : pos;
+        } else if (tie) {
+            const int te = e - less;
+            pos = te < c1 ? st1 + te : st2 + (te - c1);
+        }
+        uint4 q = uint4{0u, 0u, 0u, 0u};
+        if (e < E) q = rec_load(P.fs, gidx(P, pos, nf, __LINE__));
+        const int ci = (int)(q.w >> 16);
+        bool take = e < E;
+        if (T > need) {
+            // more entries at distance K than needed: a tie entry is taken when fewer than
+            // `need` of them have a smaller sorted index
+            int rank = 0;
+            if (E <= W) {
+                for (int f = 0; f < T; ++f) rank += rdl(ci, less + f) < ci ? 1 : 0;
+            } else {
+                for (int f = 0; f < T; ++f) {
+                    const int fp = f < c1 ? st1 + f : st2 + (f - c1);
+                    rank += (int)(rec_load(P.fs, gidx(P, fp, nf, __LINE__)).w >> 16) < ci ? 1 : 0;
+                }
+            }
+            if (tie) take = rank < need;
+        }
+        if (take) {
+            const GLOBAL_AS double *bsr = P.basis + (size_t)gidx(P, ci, P.n, __LINE__) * CCD_BASIS_STRIDE;
+            double x[7];
+#pragma unroll
+            for (int c = 0; c < 7; ++c) x[c] = bsr[c];
+            const unsigned qw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                if ((dm >> b) & 1u) {
+                    const double *c = L->coef[b];
+                    double pr = x[0] * c[0];
+#pragma unroll
+                    for (int jj = 1; jj < 7; ++jj) pr += x[jj] * c[jj];
+                    pr += c[7];
+                    const double y = (double)(int16_t)(qw[b >> 1] >> ((b & 1) * 16));
+                    const double r = y - pr;
+                    acc[b] += r * r;
+                }
+            }
+        }
+    }
+    double sb[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) sb[b] = ((dm >> b) & 1u) ? wsum(acc[b]) : 0.0;
+#pragma unroll
+    for (int t = 0; t < NB; ++t) {
+        double v = 0.0;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) v = bs[t] == b ? sb[b] : v;
+        out[t] = t < nd ? sqrt(v) / 4.0 : 0.0;
+    }
+}
+
 __device__ __forceinline__ void closest_doy_scan(Px &P, int fa, int fb, int ref_idx) {
     Lds *L = &LDS();
     const int l = lane();
@@ -2499,6 +2784,50 @@ __device__ __forceinline__ int cnt_within(const Lds *L, int nf, int u, int d) {
     const int el = bend(L, lo > 0 ? lo - 1 : 0);
     const int c = eh - (lo > 0 ? el : 0) + (lo > hi ? nf : 0);
     return d >= 730 ? nf : c;
+}
+
+// Upper bound of the closest-DOY comparison rmse of the step with reference date dref, per
+// detection band (slot order of bs), from fit_bounds' bins and blocks (per lane, nf > 24): the 24
+// closest entries lie within distance K of u (K: the smallest distance holding 24, from the bin
+// ends), so within the blocks that bins [u - K, u + K] touch.  Their float block sums are each at
+// most (n 2^-24) below the exact sum of the rounded-up terms, which bound the squares from above;
+// inflated by 2^-9 they bound the exact -- and any computed -- sum of any 24 of them.
+__device__ __forceinline__ void comp_bound(int nf, int dref, const int (&bs)[NB], int nd, double (&cb)[NB]) {
+    const Lds *L = &LDS();
+    const int u = u1461(dref);
+    int lo = 0, hi = 730;  // smallest K with cnt_within(K) >= 24
+#pragma unroll
+    for (int it = 0; it < 10; ++it) {
+        const int mid = (lo + hi) >> 1;
+        const bool ge = cnt_within(L, nf, u, mid) >= 24;
+        const bool act = lo < hi;
+        hi = act && ge ? mid : hi;
+        lo = act && !ge ? mid + 1 : lo;
+    }
+    const int K = lo;
+    // blocks of bins [u - K, u + K] (circular): one or two ascending block ranges
+    int b0 = 0, b1 = 31, c0 = 1, c1 = 0;  // ranges [b0, b1] and [c0, c1] (c0 > c1: none)
+    if (2 * K + 1 < 1461) {
+        const int x0 = u - K, x1 = u + K;
+        if (x0 < 0) {
+            b0 = (x0 + 1461) / 46; b1 = 31; c0 = 0; c1 = x1 / 46;
+        } else if (x1 > 1460) {
+            b0 = x0 / 46; b1 = 31; c0 = 0; c1 = (x1 - 1461) / 46;
+        } else {
+            b0 = x0 / 46; b1 = x1 / 46;
+        }
+    }
+    double sd[NB];
+#pragma unroll
+    for (int t = 0; t < NB; ++t) sd[t] = 0.0;
+    for (int g = b0; g <= b1; ++g)
+#pragma unroll
+        for (int t = 0; t < NB; ++t) sd[t] += t < nd ? (double)L->blk[g][bs[t]] : 0.0;
+    for (int g = c0; g <= c1; ++g)
+#pragma unroll
+        for (int t = 0; t < NB; ++t) sd[t] += t < nd ? (double)L->blk[g][bs[t]] : 0.0;
+#pragma unroll
+    for (int t = 0; t < NB; ++t) cb[t] = sqrt(sd[t] * (1.0 + 0x1p-9)) / 4.0;
 }
 
 // cs[bd] += p[s * FW + bd] for s = 0 .. cnt - 1, in order (cnt per lane).
@@ -2918,6 +3247,10 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
     int moff = 0;            // ring offset of the last evaluated peek window
     int hfa = -1, hfb = -1;  // fit window the closest-DOY buckets describe
     int nc_fit = nc;         // coefficients of the current fit
+    bool exiting = false;  // the loop ends at its top
+#ifndef CCD_BUCKET_R2
+    bool bnd_ok = false;   // fit_bounds' bins and blocks (L->hist2, L->blk) describe the current models
+#endif
     // One fit_models site for the three refits of this loop (an early step, the long-peek span
     // refit, the batched span refit): a path that needs a fit records it in fmode and continues,
     // the fit runs at the top of the next iteration, and the early / long-peek steps then resume
@@ -2926,18 +3259,39 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
     // footprint) smaller; the order of operations is unchanged.
     int fmode = 0;  // pending fit: 1 early step, 2 long-peek span refit, 3 batched refit
     for (;;) {
+        if (exiting) break;
         int ev = 0;  // single-step evaluation of this iteration: 1 early step, 2 long peek
         if (fmode) {
+#ifndef CCD_BUCKET_R2
+            // fmode 4: the current models' bounds only (a batch of more than 24 fit observations
+            // whose fit was an early step's: the first of a lookforward whose initialize window
+            // holds more than 24), then that batch again
+            if (fmode != 4) {
+#endif
             fit_models(P, fa, fb, nc_fit, fmode == 1 || fb - fa <= 24);  // rmse: from build_closest when it runs
             if (fmode == 1) {
                 have = true;
                 if (l < NB) L->comp[l] = L->rmse[l];  // early step: comparison rmse = model rmse
                 wsync();
             }
-            ev = fmode == 3 ? 0 : fmode;
+#ifndef CCD_BUCKET_R2
+            }
+            // a span refit of more than 24 observations: its rmse and the batched steps'
+            // comparison-rmse bounds from one pass over the window's residuals (the one site)
+            bnd_ok = fmode == 4 || !(fmode == 1 || fb - fa <= 24);
+            if (bnd_ok) {
+                PH_BEGIN(fbd)
+                fit_bounds(P, fa, fb, nc_fit);
+                PH_END(P, fbd, 12)  // (with build_buckets: the "closest bucket build" slot)
+            }
+#endif
+            ev = fmode == 3 || fmode == 4 ? 0 : fmode;
             fmode = 0;
         }
-        if (!ev && !(b + k < P.m || !have)) break;
+        if (!ev && !(b + k < P.m || !have)) {
+            exiting = true;
+            continue;
+        }
         if (!ev && (!have || b - a < 24)) {
             // early steps: speculative fits of the next windows, then the steps one by one
             const int nw0 = b - a;
@@ -2963,6 +3317,9 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
                     fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
                     if (installed != sp) {
                         spec_install(P, F, sp, b - a, nc);
+#ifndef CCD_BUCKET_R2
+                        bnd_ok = false;
+#endif
                         installed = sp;
                         PH_COUNT(P, 37, 1)
                     }
@@ -2987,7 +3344,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
                     b += 1;
                     sp += 1;
                 }
-                if (brk) break;
+                if (brk) exiting = true;
                 continue;
             }
             // early step: refit every step (comparison rmse = model rmse), then evaluate it
@@ -3020,7 +3377,11 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
         if (ev) {
             if (ev == 2) {
                 if (fb - fa > 24 && (hfa != fa || hfb != fb)) {
+#ifdef CCD_BUCKET_R2
                     build_closest(P, fa, fb, nc_fit);
+#else
+                    build_buckets(P, fa, fb);  // (closest_doy_scan reads the bin ends)
+#endif
                     hfa = fa;
                     hfb = fb;
                 }
@@ -3033,7 +3394,8 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
             moff = 0;
             if (chg_now) {
                 change = 1.0;
-                break;
+                exiting = true;
+                continue;
             }
             if (m0 > p.outlier_threshold) {
                 const int rm = b;
@@ -3045,6 +3407,13 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
         }
         // ---- batch of up to B steps at window starts x0 .. x0 + B - 1 (model fixed)
         const int nf = fb - fa;
+#ifndef CCD_BUCKET_R2
+        if (nf > 24 && !bnd_ok) {
+            fmode = 4;  // the bounds at the loop's top, then this batch
+            continue;
+        }
+#endif
+#ifdef CCD_BUCKET_R2
         if (nf > 24 && (hfa != fa || hfb != fb)) {
             PH_BEGIN(hb)
             build_closest(P, fa, fb, nc_fit);
@@ -3052,6 +3421,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
             hfa = fa;
             hfb = fb;
         }
+#endif
         if (nf <= 24) closest_doy_scan(P, fa, fb, b);  // every fit observation: one comp for all steps
         PH_BEGIN(cl)
         const int x0 = b, m0 = P.m;
@@ -3077,6 +3447,111 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
         }
         const unsigned long long V = bal(valid);
         bool allc = false, outj = false;
+#ifndef CCD_BUCKET_R2
+        if (nf > 24) {
+            const unsigned dm = det_mask();
+            const int nd = __builtin_popcount(dm);
+            int bs[NB];
+            unsigned rest = dm;
+#pragma unroll
+            for (int t = 0; t < NB; ++t) {
+                bs[t] = rest ? __builtin_ctz(rest) : 0;
+                rest &= rest - 1u;
+            }
+            const int drf = valid ? CDR(P, x0 + l + k - 1) : 0;  // the step's reference date (peek end)
+            // The magnitudes with the comparison rmse left out bound the true ones from above
+            // (change_magnitude divides by max(vario, comp) >= vario; division, multiplication,
+            // squares and sums are monotone under round-to-nearest): a step whose upper bound has
+            // a peek magnitude <= the change threshold and a first one <= the outlier threshold
+            // is a plain step, exactly as with its comp (~95 % of steps).  The others -- nearly
+            // all true outliers -- get a lower bound too, from an upper bound of comp
+            // (comp_bound: the squared residuals of the fit-window blocks around the step's day
+            // of year, fit_bounds); a step whose two bounds agree on both tests is decided.  The
+            // C3 tile mix leaves ~0.1 % of its steps to the exact comparison rmse below.
+            bool und = false, au = false, ou = false;
+            PH_BEGIN(mgu)
+            if (valid) {
+                double iu[NB];
+                bool vz = false;  // a zero vario: 1 / vario is infinite (r = 0 would give NaN) -- no bound
+#pragma unroll
+                for (int t = 0; t < NB; ++t) {
+                    const double vr = L->vario[bs[t]];
+                    iu[t] = t < nd ? 1.0 / vr : 0.0;  // (a NaN vario: NaN, as with any comp)
+                    vz = vz || (t < nd && vr == 0.0);
+                }
+                if (nd <= 5) peek_mags<5>(bs, iu, k, au, ou);
+                else peek_mags<NB>(bs, iu, k, au, ou);
+                und = vz || au || ou;
+            }
+            unsigned long long Um = bal(und);
+            if (Um) {
+                if (und) {
+                    double cbv[NB];
+                    comp_bound(nf, drf, bs, nd, cbv);
+                    double il[NB];
+                    bool vz = false;
+#pragma unroll
+                    for (int t = 0; t < NB; ++t) {
+                        const double vr = L->vario[bs[t]], cb = cbv[t];
+                        const double rm = (vr != vr || cb != cb) ? __builtin_nan("") : (vr > cb ? vr : cb);
+                        il[t] = t < nd ? 1.0 / rm : 0.0;
+                        vz = vz || (t < nd && vr == 0.0);
+                    }
+                    bool al = false, ol = false;
+                    if (nd <= 5) peek_mags<5>(bs, il, k, al, ol);
+                    else peek_mags<NB>(bs, il, k, al, ol);
+                    if (!vz && al == au && ol == ou) {
+                        allc = au;
+                        outj = ou;
+                        und = false;
+                    }
+                }
+                Um = bal(und);
+            }
+            PH_END(P, mgu, 15)
+            if (Um) {
+                // the undecided steps in order, each resolved exactly; once a step below the next
+                // one is known to end the batch (change or span refit, from the steps below it,
+                // all exact by then) the rest lie past the batch's first terminating step and
+                // cannot change its outcome (left undecided as plain steps: allc = outj = false)
+                PH_BEGIN(cmp)
+                int nres = 0;
+                for (unsigned long long mm = Um; mm; mm &= mm - 1ull) {
+                    const int x = __builtin_ctzll(mm);
+                    const unsigned long long Ok = bal(valid && outj);
+                    const unsigned long long lw = (V & ~Ok) & ((1ull << l) - 1ull);
+                    const int lkk = lw ? 63 - __clzll(lw) : 0;
+                    const int dsh = shf(dj, lkk);
+                    const int dlk = lw ? dsh : dprev;
+                    const bool trg = valid && ((double)dlk - (double)da) >= 1.33 * fit_span;
+                    if (bal(l < x && (trg || allc))) break;
+                    if (hfa != fa || hfb != fb) {
+                        PH_BEGIN(hb)
+                        build_buckets(P, fa, fb);
+                        PH_END(P, hb, 12)
+                        hfa = fa;
+                        hfb = fb;
+                    }
+                    double o[NB];
+                    coop_comp(P, nf, rdl(drf, x), bs, nd, o);
+                    ++nres;
+                    if (l == x) {
+                        double irm[NB];
+#pragma unroll
+                        for (int t = 0; t < NB; ++t) {
+                            const double vr = L->vario[bs[t]], cr = o[t];
+                            const double rm = (vr != vr || cr != cr) ? __builtin_nan("") : (vr > cr ? vr : cr);
+                            irm[t] = t < nd ? 1.0 / rm : 0.0;
+                        }
+                        if (nd <= 5) peek_mags<5>(bs, irm, k, allc, outj);
+                        else peek_mags<NB>(bs, irm, k, allc, outj);
+                    }
+                }
+                PH_COUNT(P, 21, nres)  // (slot of comp_lane's search timer, unused on this path)
+                PH_END(P, cmp, 14)
+            }
+        } else
+#endif
         if (valid) {
             // comparison rmse per detection band: cs[s] for the s-th detection band bs[s]
             const unsigned dm = det_mask();
@@ -3155,7 +3630,8 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
         if (change_here) {
             b = peek_start;
             change = 1.0;
-            break;
+            exiting = true;
+            continue;
         }
         b = x0 + xs - R;
         if (Tm) {

@@ -29,6 +29,9 @@ for i, n in enumerate(counts):
     out[n] = dc[8 + 16 + i]
 for i, n in enumerate(['spec early fits (CD)', 'closest: search', 'closest: run sum', 'closest: ties']):
     out[n] = dc[8 + 20 + i] / tot
+# default kernel (bucket records + bounded magnitudes): slot 21 counts the steps whose comparison
+# rmse was computed (coop_comp); comp_lane's sub-phase timers 21-23 belong to the CCD_BUCKET_R2 build
+out['steps with comparison rmse (coop_comp)'] = dc[8 + 21]
 for i, n in enumerate(['batches ne<=16', 'batches ne<=32', 'batch valid lanes', 'batches without terminal step',
                        'wave fits at max_iter', 'wave sweeps (single fits)', 'wave sweeps in max_iter fits',
                        'compaction rows scanned']):
