@@ -63,9 +63,9 @@ struct __attribute__((aligned(16))) Lds {
             double G[8][8];
             double Q[8][8];  // Q[j][band] = Xc_j . yc_band
         };
-        // lookforward between two fits (G / Q are rebuilt at every fit): per block of 46 bins of
-        // u = 4 t mod 1461, the fit window's squared residuals of the current models summed per
-        // band in float, every term rounded up (fit_bounds)
+        // lookforward between two fits (G / Q are rebuilt at every fit): per band, the inclusive
+        // prefix over blocks of 46 bins of u = 4 t mod 1461 of the fit window's squared residuals
+        // of the current models, in float, every term rounded up (fit_bounds)
         float blk[32][8];
     };
     double YY[8];
@@ -359,6 +359,19 @@ __device__ __forceinline__ int wscan_incl(int v XL) {
     v += (row & 1) ? t15 : 0;
     const int t31 = __builtin_amdgcn_update_dpp(0, v, 0x143, 0xF, 0xF, false);
     v += (row & 2) ? t31 : 0;
+    return v;
+}
+// Inclusive prefix sum of a float over each 32-lane half of the wave, in DPP only (wscan_incl
+// without the row_bcast:31 step that carries the first half into the second).
+__device__ __forceinline__ float fscan32(float v XL) {
+    EXEC_FULL();
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xF, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x112, 0xF, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x114, 0xF, 0xF, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x118, 0xF, 0xF, false));
+    const int row = (int)__lane_id() >> 4;
+    const float t15 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xF, 0xF, false));
+    v += (row & 1) ? t15 : 0.0f;
     return v;
 }
 // value of v in a (wave-uniform) lane, as a scalar
@@ -2574,6 +2587,16 @@ __device__ __forceinline__ void fit_bounds(const Px &P, int fa, int fb, int k) {
             }
         }
     }
+    wsync();
+    // per band, the block sums -> their inclusive prefix over the 32 blocks (two bands a pass,
+    // one per 32-lane half; float, the rounding is covered in comp_bound)
+#pragma unroll
+    for (int b2 = 0; b2 < NB; b2 += 2) {
+        const int b = b2 + (l >> 5), g = l & 31;
+        float v = b < NB ? L->blk[g][b] : 0.0f;
+        v = fscan32(v);
+        if (b < NB) L->blk[g][b] = v;
+    }
     const double den = (double)(nf - (ARGS().p.rmse_dof ? k : 0));
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
@@ -2817,17 +2840,21 @@ __device__ __forceinline__ void comp_bound(int nf, int dref, const int (&bs)[NB]
             b0 = x0 / 46; b1 = x1 / 46;
         }
     }
-    double sd[NB];
+    // L->blk holds per band the inclusive prefix over the blocks (fit_bounds): a range is two
+    // reads; the prefixes' float rounding (< 2.5e-4 of the total for <= 4096 terms) is covered by
+    // 2^-10 of the total
 #pragma unroll
-    for (int t = 0; t < NB; ++t) sd[t] = 0.0;
-    for (int g = b0; g <= b1; ++g)
-#pragma unroll
-        for (int t = 0; t < NB; ++t) sd[t] += t < nd ? (double)L->blk[g][bs[t]] : 0.0;
-    for (int g = c0; g <= c1; ++g)
-#pragma unroll
-        for (int t = 0; t < NB; ++t) sd[t] += t < nd ? (double)L->blk[g][bs[t]] : 0.0;
-#pragma unroll
-    for (int t = 0; t < NB; ++t) cb[t] = sqrt(sd[t] * (1.0 + 0x1p-9)) / 4.0;
+    for (int t = 0; t < NB; ++t) {
+        double sd = 0.0;
+        if (t < nd) {
+            const int b = bs[t];
+            const double tot = (double)L->blk[31][b];
+            sd = (double)L->blk[b1][b] - (b0 > 0 ? (double)L->blk[b0 - 1][b] : 0.0);
+            if (c0 <= c1) sd += (double)L->blk[c1][b] - (c0 > 0 ? (double)L->blk[c0 - 1][b] : 0.0);
+            sd += 0x1p-10 * tot;
+        }
+        cb[t] = sqrt(sd * (1.0 + 0x1p-9)) / 4.0;
+    }
 }
 
 // cs[bd] += p[s * FW + bd] for s = 0 .. cnt - 1, in order (cnt per lane).
