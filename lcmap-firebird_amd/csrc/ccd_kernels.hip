@@ -2500,6 +2500,9 @@ __device__ __forceinline__ void build_buckets(const Px &P, int fa, int fb) {
     gsync();  // the records are read by other lanes
 }
 
+#ifndef CCD_FBU
+#define CCD_FBU 2  // chunks of 64 observations per round of fit_bounds' residual pass
+#endif
 // Per fit (lookforward, more than 24 fit observations), once it is needed: lasso.fitted_model's
 // rmse of the current models over the fit window [fa, fb) -- the same arithmetic, per-lane order
 // and wave reduction as build_closest's (lane l sums observations fa + l, fa + l + 64, ...), so
@@ -2511,20 +2514,22 @@ __device__ __forceinline__ void fit_bounds(const Px &P, int fa, int fb, int k) {
     const int l = lane();
     const int nf = fb - fa;
     const unsigned dm = det_mask();
-    build_hist(P, fa, fb);
-    bins_prefix(true);
+    // the bin counts (L->hist2) are gathered in the residual pass (one pass over the window's
+    // dates, not two) and turned into bin ends after it
+    for (int i = l; i < 732; i += W) L->hist2[i] = 0u;
     float *bz = &L->blk[0][0];
     for (int i = l; i < 32 * 8; i += W) bz[i] = 0.0f;
     wsync();
     double ssq[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) ssq[b] = 0.0;
-    // two chunks per round, software-pipelined as build_closest: the next round's rows and dates
+    // FU chunks per round, software-pipelined as build_closest: the next round's rows and dates
     // load while this round's design rows load (lane l still adds fa + l, fa + l + 64, ... in order)
-    uint4 qn[2];
-    int dn[2];
+    constexpr int FU = CCD_FBU;
+    uint4 qn[FU];
+    int dn[FU];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < FU; ++u) {
         const int i = fa + u * W + l;
         qn[u] = uint4{0u, 0u, 0u, 0u};
         dn[u] = 0;
@@ -2533,25 +2538,25 @@ __device__ __forceinline__ void fit_bounds(const Px &P, int fa, int fb, int k) {
             dn[u] = CDR(P, i);
         }
     }
-    for (int i0 = fa; i0 < fb; i0 += 2 * W) {
-        uint4 qv[2];
-        int dt[2];
-        double xv[2][7];
+    for (int i0 = fa; i0 < fb; i0 += FU * W) {
+        uint4 qv[FU];
+        int dt[FU];
+        double xv[FU][7];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < FU; ++u) {
             qv[u] = qn[u];
             dt[u] = dn[u];
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < FU; ++u) {
             const int i = i0 + u * W + l;
             const GLOBAL_AS double *bs = P.basis + (size_t)gidx(P, i < fb ? (int)(qv[u].w >> 16) : 0, P.n, __LINE__) * CCD_BASIS_STRIDE;
 #pragma unroll
             for (int c = 0; c < 7; ++c) xv[u][c] = bs[c];
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int i = i0 + (2 + u) * W + l;
+        for (int u = 0; u < FU; ++u) {
+            const int i = i0 + (FU + u) * W + l;
             qn[u] = uint4{0u, 0u, 0u, 0u};
             dn[u] = 0;
             if (i < fb) {
@@ -2560,10 +2565,12 @@ __device__ __forceinline__ void fit_bounds(const Px &P, int fa, int fb, int k) {
             }
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < FU; ++u) {
             const int i = i0 + u * W + l;
             if (i >= fb) continue;
-            const int blk = u1461(dt[u]) / 46;
+            const int ub = u1461(dt[u]);
+            const int blk = ub / 46;
+            atomicAdd(&L->hist2[ub >> 1], 1u << ((ub & 1) * 16));
             const double *x = xv[u];
             const unsigned qw[4] = {qv[u].x, qv[u].y, qv[u].z, qv[u].w};
 #pragma unroll
@@ -2588,6 +2595,7 @@ __device__ __forceinline__ void fit_bounds(const Px &P, int fa, int fb, int k) {
         }
     }
     wsync();
+    bins_prefix(true);
     // per band, the block sums -> their inclusive prefix over the 32 blocks (two bands a pass,
     // one per 32-lane half; float, the rounding is covered in comp_bound)
 #pragma unroll
