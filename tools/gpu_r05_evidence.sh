@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-5 evidence at HEAD (developer tool, GPU box): GPU suite, smoke, default bench, the
 # single-context rocprofv3 kernel-stats pass + PMC passes of the C3 resident workload, the C5 PMC
-# passes, and (PARITY=1) the 250k-pixel tile parity run.  Each GPU step has its own time limit;
+# passes (the C5 PMC passes and the tile parity run: tools/gpu_r05_parity.sh).  Each GPU step has its own time limit;
 # the first failure ends the session.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
@@ -16,9 +16,4 @@ timeout -k 10 500 python -u bench.py > gpurun_out/${T}_bench.json 2> gpurun_out/
 python -c "import json; d=json.load(open('gpurun_out/${T}_bench.json')); print('tile', round(d['value']), 'resident', round(d['value_resident']), 'frac', round(d['roofline']['frac'],4), 'ms', round(d['roofline']['kernel_ms_per_launch'],2), d['tile']['parity_sample']['int_mismatches'], d['tile']['parity_sample']['float_mismatches'])"
 fi
 PMC=1 bash tools/gpu_evidence_stats.sh ${T}_stats || { echo "stats/pmc failed"; exit 1; }
-CONFIG=5 bash tools/gpu_pmc.sh ${T}_c5_pmc || { echo "c5 pmc failed"; cat gpurun_out/${T}_c5_pmc_rc.txt; exit 1; }
-echo c5 pmc ok
-if [ -n "$PARITY" ]; then
-timeout -k 10 900 python -u tools/tile_parity.py --batch 6 --out gpurun_out/${T}_tile_parity.json > gpurun_out/${T}_tile_parity.log 2>&1 || { echo "parity rc=$?"; tail -20 gpurun_out/${T}_tile_parity.log; exit 1; }
-tail -1 gpurun_out/${T}_tile_parity.log
-fi
+echo stats pmc ok
