@@ -3622,7 +3622,8 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
                 // all exact by then) the rest lie past the batch's first terminating step and
                 // cannot change its outcome (left undecided as plain steps: allc = outj = false)
                 PH_BEGIN(cmp)
-                int nres = 0;
+                int nres = 0;  // (counted in the diagnostic build)
+                (void)nres;
                 for (unsigned long long mm = Um; mm; mm &= mm - 1ull) {
                     const int x = __builtin_ctzll(mm);
                     const unsigned long long Ok = bal(valid && outj);
