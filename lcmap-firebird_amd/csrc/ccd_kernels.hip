@@ -86,7 +86,6 @@ struct __attribute__((aligned(16))) Lds {
     union {                // Tmask (initialize) and the closest-DOY buckets (lookforward) never overlap
         uint32_t hist2[732];   // closest-DOY: fit-window counts per (4 t mod 1461) bin, 2 x u16 per word
         uint16_t hist16[1464]; // the same bins read one u16 at a time (ds_read_u16: no shift / mask)
-        double sav[NB][9];     // lookforward's end: the detection bands' speculative models (coef, rmse)
         struct {
             uint32_t tflag[MAXW];  // Tmask outlier flags of the current window
             double tchol[5][5];    // Tmask: Cholesky factor of the unweighted normal matrix
@@ -3048,27 +3047,12 @@ struct SpecFit {
 // index of (i, j), i <= j, in a row-major upper triangle of SPEC_PC columns
 __host__ __device__ constexpr int ut(int i, int j) { return i * SPEC_PC - i * (i - 1) / 2 + (j - i); }
 
-// Lane (window v, slot s) of a speculative fit over the bands of mask bm, nb lanes per window:
-// v = l / nb, band = the s-th set bit of bm (s >= popcount(bm): no band, the lane idles)
-__device__ __forceinline__ int spec_band(unsigned bm, int nb, int l, int &v, bool &has) {
-    v = l / nb;
-    const int s = l - v * nb;
-    int band = 0;
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-        band = (((bm >> b) & 1u) && __builtin_popcount(bm & ((1u << b) - 1u)) == s) ? b : band;
-    has = s < __builtin_popcount(bm);
-    return band;
-}
-
-__device__ __forceinline__ void spec_fits(Px &P, int a, int nw0, int V, SpecFit &F, unsigned bm, int nb) {
+__device__ __forceinline__ void spec_fits(Px &P, int a, int nw0, int V, SpecFit &F) {
     const ccdgpu_params &p = ARGS().p;
     Lds *L = &LDS();
     const int l = lane();
-    int v;
-    bool has;
-    const int band = spec_band(bm, nb, l, v, has);
-    const bool act = has && v < V;
+    const int v = l >> 3, band = l & 7;
+    const bool act = band < NB && v < V;
     const int nv = nw0 + v;       // rows of this lane's window
     const int R = nw0 + V - 1;    // rows staged (<= 23 < TR)
     const int t0 = CDR(P, a);
@@ -3084,7 +3068,7 @@ __device__ __forceinline__ void spec_fits(Px &P, int a, int nw0, int V, SpecFit 
         for (int bd = 0; bd < NB; ++bd) r[8 + bd] = (double)((int)cw.v[bd] - (int)c0.v[bd]);
     }
     wsync();
-    const int yb = band;
+    const int yb = band < NB ? band : 0;
     const int y0 = (int)c0.v[yb];
     // raw sums of the lane's window in shifted coordinates (exact integer shifts)
     double sx[SPEC_PC], sxy[SPEC_PC], sxx[ut(SPEC_PC - 1, SPEC_PC - 1) + 1];
@@ -3229,13 +3213,11 @@ __device__ __forceinline__ void spec_fits(Px &P, int a, int nw0, int V, SpecFit 
 }
 
 // Models of speculative window s (lanes (s, band)) into the model slots of LDS; comp = rmse.
-__device__ __forceinline__ void spec_install(Px &P, const SpecFit &F, int s, int nw, int kc, unsigned bm, int nb) {
+__device__ __forceinline__ void spec_install(Px &P, const SpecFit &F, int s, int nw, int kc) {
     Lds *L = &LDS();
     const int l = lane();
-    int v;
-    bool has;
-    const int band = spec_band(bm, nb, l, v, has);
-    if (v == s && has) {
+    const int v = l >> 3, band = l & 7;
+    if (v == s && band < NB) {
 #pragma unroll
         for (int i = 0; i < SPEC_PC; ++i) L->coef[band][i] = F.w[i];
         L->coef[band][5] = 0.0;
@@ -3284,28 +3266,6 @@ __device__ __forceinline__ void peek_mags(const int (&bs)[NB], const double (&ir
     }
 }
 
-// A segment that ends on a speculatively fitted model (detection bands only) gets the other
-// bands' models of its window from the loop's fit site (fmode 5: a fit of all bands, the detection
-// bands' speculative models put back after it); then their residuals at the final peek (logical
-// peek_start + jj, ring offset moff + jj; resid_at = the arithmetic of eval_peek and ring_rows)
-// for the segment's magnitudes.
-__device__ __forceinline__ void ring_other_bands(Px &P, int k, int peek_start, int moff) {
-    Lds *L = &LDS();
-    const int l = lane();
-    const unsigned om = 0x7Fu & ~det_mask();
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        if (!((om >> b) & 1u)) continue;
-        for (int jj = l; jj < k; jj += W) {
-            const double r = resid_at(P, b, peek_start + jj);
-            const int o = moff + jj;
-            if (o < PSTR) PRES(L)[b * PSTR + o] = r;
-            else ring_ovf(P)[b * POVF + o - PSTR] = r;
-        }
-    }
-    wsync();
-}
-
 __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
     const ccdgpu_params &p = ARGS().p;
     Lds *L = &LDS();
@@ -3323,7 +3283,6 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
     int hfa = -1, hfb = -1;  // fit window the closest-DOY buckets describe
     int nc_fit = nc;         // coefficients of the current fit
     bool exiting = false;  // the loop ends at its top
-    bool full7 = true;     // L->coef / L->rmse hold every band's model (not only the detection bands')
 #ifndef CCD_BUCKET_R2
     bool bnd_ok = false;   // fit_bounds' bins and blocks (L->hist2, L->blk) describe the current models
 #endif
@@ -3335,35 +3294,16 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
     // footprint) smaller; the order of operations is unchanged.
     int fmode = 0;  // pending fit: 1 early step, 2 long-peek span refit, 3 batched refit
     for (;;) {
-        if (exiting && full7) break;
-        if (exiting) fmode = 5;  // the other bands' models of the final (speculative) window first
+        if (exiting) break;
         int ev = 0;  // single-step evaluation of this iteration: 1 early step, 2 long peek
         if (fmode) {
-            if (fmode == 5 && l < NB) {  // keep the detection bands' speculative models
-#pragma unroll
-                for (int j = 0; j < 8; ++j) L->sav[l][j] = L->coef[l][j];
-                L->sav[l][8] = L->rmse[l];
-            }
-            wsync();
 #ifndef CCD_BUCKET_R2
             // fmode 4: the current models' bounds only (a batch of more than 24 fit observations
             // whose fit was an early step's: the first of a lookforward whose initialize window
             // holds more than 24), then that batch again
             if (fmode != 4) {
 #endif
-            fit_models(P, fa, fb, nc_fit, fmode == 1 || fmode == 5 || fb - fa <= 24);  // rmse: from build_closest when it runs
-            full7 = true;
-            if (fmode == 5) {
-                if (l < NB && ((det_mask() >> l) & 1u)) {
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) L->coef[l][j] = L->sav[l][j];
-                    L->rmse[l] = L->sav[l][8];
-                }
-                wsync();
-                ring_other_bands(P, k, peek_start, moff);
-                fmode = 0;
-                continue;  // (exiting)
-            }
+            fit_models(P, fa, fb, nc_fit, fmode == 1 || fb - fa <= 24);  // rmse: from build_closest when it runs
             if (fmode == 1) {
                 have = true;
                 if (l < NB) L->comp[l] = L->rmse[l];  // early step: comparison rmse = model rmse
@@ -3388,27 +3328,16 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
             continue;
         }
         if (!ev && (!have || b - a < 24)) {
-            // early steps: speculative fits of the next windows, then the steps one by one.  Only
-            // the detection bands are fitted ahead (5 lanes per window: up to 12 windows, the whole
-            // early phase of a segment in one call): the other bands' models enter neither test
-            // and are fitted for the one window the segment ends on, if it ends on one of these
-            // (spec_complete)
-#ifdef CCD_SPEC_ALL7
-            const unsigned sbm = 0x7Fu;
-            const int snb = 8;
-#else
-            const unsigned sbm = det_mask();
-            const int snb = __builtin_popcount(sbm);
-#endif
+            // early steps: speculative fits of the next windows, then the steps one by one
             const int nw0 = b - a;
             int V = 24 - nw0;
-            V = V > W / snb ? W / snb : V;
+            V = V > 8 ? 8 : V;
             V = V > P.m - b + 1 ? P.m - b + 1 : V;  // staged rows stay inside the period
             while (V > 1 && num_coefs(p, nw0 + V - 1) - 1 > SPEC_PC) --V;
             if (V >= 1 && num_coefs(p, nw0) - 1 <= SPEC_PC) {
                 PH_BEGIN(sf)
                 SpecFit F;
-                spec_fits(P, a, nw0, V, F, sbm, snb);
+                spec_fits(P, a, nw0, V, F);
                 PH_END(P, sf, 20)
                 int sp = 0, valid = V - 1, installed = -1;
                 bool brk = false;
@@ -3422,8 +3351,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
                     fb = b;
                     fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
                     if (installed != sp) {
-                        spec_install(P, F, sp, b - a, nc, sbm, snb);
-                        full7 = sbm == 0x7Fu;
+                        spec_install(P, F, sp, b - a, nc);
 #ifndef CCD_BUCKET_R2
                         bnd_ok = false;
 #endif
