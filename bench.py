@@ -403,8 +403,8 @@ def resident_leg(args, cfg, rank, world, device, dist, batch=None):
             'unit': 'TFLOP/s',
             'frac': achieved_tf / FP64_PEAK_TFLOPS,
             'traffic': traffic,
-            'kernel': {'w1': 'ccd_detect', 'w2': 'ccd_detect_w2', 'w4': 'ccd_detect_w4'}.get(
-                os.environ.get('CCDGPU_KERNEL', 'w3'), 'ccd_detect_w3'),
+            'kernel': {'w1': 'ccd_detect', 'w2': 'ccd_detect_w2', 'w3': 'ccd_detect_w3'}.get(
+                os.environ.get('CCDGPU_KERNEL', 'w4'), 'ccd_detect_w4'),
             'workload_key': workload_key,
             'traffic_note': 'traffic = HBM bytes per launch from rocprofv3 --pmc (profiles/pmc_detect.json, same workload_key), else null',
             'kernel_ms_per_launch': launch_ms,

@@ -4119,8 +4119,9 @@ __device__ __forceinline__ void detect_body() {
 }
 
 // Four register budgets of the same body: 1 wave/SIMD (no spills), 2, 3 and 4 waves/SIMD (256,
-// 168 and 128 VGPRs, spills growing).  The host picks one (CCDGPU_KERNEL=w1..w4; default w3, the
-// fastest: w4's spills cost more than its 4th wave gains).
+// 168 and 128 VGPRs, spills growing).  The host picks one (CCDGPU_KERNEL=w1..w4; default w4, the
+// fastest since round 5: C3 185.5 vs 193.0 ms per launch, C5 600 vs 614 ms -- its fourth wave hides
+// more latency than its extra spills cost).
 // (arg_slot: the c_args slot of the launching context, read by ARGS() from the kernarg segment)
 __global__ __launch_bounds__(64) __attribute__((flatten)) void ccd_detect(int arg_slot) { detect_body(); }
 __global__ __launch_bounds__(64, 2) __attribute__((flatten)) void ccd_detect_w2(int arg_slot) { detect_body(); }

@@ -177,7 +177,7 @@ struct ccdgpu_ctx {
     int device = 0;
     int n_cu = 0;
     int slots_per_cu = 0;
-    int variant = 3;  // detection kernel register budget: 1..4 waves/SIMD (CCDGPU_KERNEL=w1..w4)
+    int variant = 4;  // detection kernel register budget: 1..4 waves/SIMD (CCDGPU_KERNEL=w1..w4)
     int poison = 0;   // CCDGPU_POISON=1: LDS and slot scratch filled with NaN bytes per pixel (test mode)
     int arg_slot = -1;  // this context's launch-argument slot in constant memory
     hipStream_t stream = nullptr;
@@ -496,7 +496,7 @@ int ccdgpu_init_copy_cus(int device, int copy_cus, ccdgpu_ctx **out) {
         return fail(CCDGPU_EINVAL, "more than " + std::to_string(CCD_ARG_SLOTS) + " live contexts in this process");
     }
     c->slots_per_cu = 16;
-    c->variant = ccdk_period_in_lds() ? 1 : 3;
+    c->variant = ccdk_period_in_lds() ? 1 : 4;
     if (const char *v = std::getenv("CCDGPU_KERNEL")) {
         if (v[0] == 'w' && v[1] >= '1' && v[1] <= '4' && v[2] == 0) c->variant = v[1] - '0';
     }

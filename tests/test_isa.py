@@ -100,6 +100,7 @@ def test_product_isa_is_clean():
     r = subprocess.run([sys.executable, os.path.join(TOOLS, 'dpp_hazards.py'), ISA], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-2000:]
     # the build carries the fix: no `if` is lowered without saving EXEC
-    out = subprocess.run([sys.executable, os.path.join(TOOLS, 'endcf_check.py'), ISA, 'ccd_detect_w3'],
-                         capture_output=True, text=True).stdout
-    assert ': 0 ifs without an EXEC save' in out, out
+    for kern in ('ccd_detect_w4', 'ccd_detect_w3'):  # the product's 4-waves kernel, and w3
+        out = subprocess.run([sys.executable, os.path.join(TOOLS, 'endcf_check.py'), ISA, kern],
+                             capture_output=True, text=True).stdout
+        assert ': 0 ifs without an EXEC save' in out, out
