@@ -277,6 +277,8 @@ __device__ __forceinline__ uint4 crow4(const Px &P, int j, int line) {
 #define CROW4(P, j) crow4(P, (j), __LINE__)
 #define CROW(P, j) crow(P, (j), __LINE__)
 #define CDR(P, j) cdr(P, (j), __LINE__)
+// the date of a row whose index is wave-uniform, as a scalar (see uni)
+#define CDRU(P, j) uni(cdr(P, (j), __LINE__))
 #define CIR(P, j) cir(P, (j), __LINE__)
 #define CVR(P, b, j) cvr(P, (b), (j), __LINE__)
 
@@ -373,6 +375,14 @@ __device__ __forceinline__ float fscan32(float v XL) {
     const float t15 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xF, 0xF, false));
     v += (row & 1) ? t15 : 0.0f;
     return v;
+}
+// a wave-uniform value (every lane holds the same) as a scalar: the compiler's divergence
+// analysis cannot see through lane shuffles and DPP reductions, and a value it takes for
+// divergent lives in a VGPR (two for a pointer) -- and so does everything computed from it
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ unsigned long long uni(unsigned long long v) {
+    return ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+           (unsigned)__builtin_amdgcn_readfirstlane((int)v);
 }
 // value of v in a (wave-uniform) lane, as a scalar
 __device__ __forceinline__ int rdl(int v, int src XL) {
@@ -615,7 +625,7 @@ __device__ __forceinline__ void gram_accumulate(Px &P, int a, int b) {
     int from = P.acc_b;
     if (!(P.acc_a == a && P.acc_b <= b)) {
         P.acc_a = a;
-        P.acc_t0 = CDR(P, a);
+        P.acc_t0 = CDRU(P, a);
         if (l < NB) L->y0[l] = (int)CVR(P, l, a);
         L->S[l] = 0.0;
         if (l + W < 98) L->S[l + W] = 0.0;
@@ -1061,7 +1071,7 @@ __device__ __forceinline__ void emit(Px &P, int sday, int eday, int bday, int co
     const int l = lane();
     unsigned long long slot = 0;
     if (l == 0) slot = atomicAdd(&A.counters[1], 1ull);
-    slot = shf((unsigned long long)slot, 0);
+    slot = uni(slot);  // lane 0's
     if (slot >= (unsigned long long)A.pool_cap) {
         if (l == 0) atomicOr(&A.counters[3], 1ull);
         P.nseg++;
@@ -1345,7 +1355,7 @@ __device__ __forceinline__ void adjust_peek(Px &P) {
         // PEEK_SIZE can exceed it: the pixel is reported (the call fails with CCDGPU_EOVERFLOW)
         // and finished with the largest supported peek so the launch still drains.
         if (adj > (double)CCDGPU_MAX_PEEK && lane() == 0) atomicMin(&ARGS().counters[7], (unsigned long long)P.gpix);
-        P.peek = adj > (double)CCDGPU_MAX_PEEK ? CCDGPU_MAX_PEEK : (int)adj;
+        P.peek = uni(adj > (double)CCDGPU_MAX_PEEK ? CCDGPU_MAX_PEEK : (int)adj);
         if (lane() == 0) LDS().chg = ARGS().thr_table[P.peek];
     }
 }
@@ -2109,7 +2119,7 @@ __device__ __forceinline__ bool initialize(Px &P, int &wa, int &wb) {
     int a = wa, b = wb;
     bool ok = false;
     while (b + p.meow_size < P.m) {
-        if (CDR(P, b - 1) - CDR(P, a) < p.day_delta) { b += 1; continue; }
+        if (CDRU(P, b - 1) - CDRU(P, a) < p.day_delta) { b += 1; continue; }
         PH_BEGIN(tm)
         const int cnt = tmask(P, a, b);
         PH_END(P, tm, 3)
@@ -2129,7 +2139,7 @@ __device__ __forceinline__ bool initialize(Px &P, int &wa, int &wb) {
                 last = la;
             }
         }
-        if (CDR(P, a + last) - CDR(P, a + first) < p.day_delta || nw - cnt < p.meow_size) { b += 1; continue; }
+        if (CDRU(P, a + last) - CDRU(P, a + first) < p.day_delta || nw - cnt < p.meow_size) { b += 1; continue; }
         if (cnt) {
             const int aa = a, bb = b;
             compact_drop(P, a, bb, [&](int j) { return tflag_at(L, j - aa); });
@@ -3047,7 +3057,11 @@ struct SpecFit {
 // index of (i, j), i <= j, in a row-major upper triangle of SPEC_PC columns
 __host__ __device__ constexpr int ut(int i, int j) { return i * SPEC_PC - i * (i - 1) / 2 + (j - i); }
 
+#ifdef CCD_SPEC_CALL
+__device__ __attribute__((noinline)) void spec_fits(Px &P, int a, int nw0, int V, SpecFit &F) {
+#else
 __device__ __forceinline__ void spec_fits(Px &P, int a, int nw0, int V, SpecFit &F) {
+#endif
     const ccdgpu_params &p = ARGS().p;
     Lds *L = &LDS();
     const int l = lane();
@@ -3055,7 +3069,7 @@ __device__ __forceinline__ void spec_fits(Px &P, int a, int nw0, int V, SpecFit 
     const bool act = band < NB && v < V;
     const int nv = nw0 + v;       // rows of this lane's window
     const int R = nw0 + V - 1;    // rows staged (<= 23 < TR)
-    const int t0 = CDR(P, a);
+    const int t0 = CDRU(P, a);
     const CRow c0 = CROW(P, a);   // value shifts: the window's first observation
     if (l < R) {
         const CRow cw = CROW(P, a + l);
@@ -3277,7 +3291,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
     bool have = false;
     double change = 0.0;
     int nc = p.coef_min;
-    double fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
+    int fit_span = CDRU(P, b - 1) - CDRU(P, a);  // days (wave-uniform)
     int peek_start = b;
     int moff = 0;            // ring offset of the last evaluated peek window
     int hfa = -1, hfb = -1;  // fit window the closest-DOY buckets describe
@@ -3349,7 +3363,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
                     peek_start = b;
                     fa = a;
                     fb = b;
-                    fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
+                    fit_span = CDRU(P, b - 1) - CDRU(P, a);
                     if (installed != sp) {
                         spec_install(P, F, sp, b - a, nc);
 #ifndef CCD_BUCKET_R2
@@ -3387,7 +3401,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
             peek_start = b;
             fa = a;
             fb = b;
-            fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
+            fit_span = CDRU(P, b - 1) - CDRU(P, a);
             nc_fit = nc;
             fmode = 1;
             continue;
@@ -3398,9 +3412,9 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
             // test, comparison rmse from the 24 closest-DOY fit observations of the peek end.
             nc = num_coefs(p, b - a);
             peek_start = b;
-            const double span = (double)CDR(P, b - 1) - (double)CDR(P, a);
+            const int span = CDRU(P, b - 1) - CDRU(P, a);
             ev = 2;
-            if (span >= 1.33 * fit_span) {
+            if ((double)span >= 1.33 * (double)fit_span) {
                 fa = a;
                 fb = b;
                 fit_span = span;
@@ -3465,8 +3479,8 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
         PH_END(P, rr, 13)
         PH_COUNT(P, 17, 1)
         bool valid = l < B && x0 + l + k < m0;
-        const int da = CDR(P, a);
-        const int dprev = CDR(P, x0 - 1);
+        const int da = CDRU(P, a);
+        const int dprev = CDRU(P, x0 - 1);
         const int dj = valid ? CDR(P, x0 + l) : 0;
         {
             // Steps past the first span-test refit are never executed.  Without removals step l's
@@ -3475,7 +3489,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
             // lanes more than 2 steps past it are left out (with more removals before it the batch
             // ends there without a terminal step and the next one continues).
             const int dp = shf(dj, l > 0 ? l - 1 : 0);
-            const bool t0 = valid && ((double)(l > 0 ? dp : dprev) - (double)da) >= 1.33 * fit_span;
+            const bool t0 = valid && ((double)(l > 0 ? dp : dprev) - (double)da) >= 1.33 * (double)fit_span;
             const unsigned long long T0 = bal(t0);
             const int lim = T0 ? __ffsll((long long)T0) + 1 : W;  // first such step + 2
             valid = valid && l <= lim;
@@ -3559,7 +3573,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
                     const int lkk = lw ? 63 - __clzll(lw) : 0;
                     const int dsh = shf(dj, lkk);
                     const int dlk = lw ? dsh : dprev;
-                    const bool trg = valid && ((double)dlk - (double)da) >= 1.33 * fit_span;
+                    const bool trg = valid && ((double)dlk - (double)da) >= 1.33 * (double)fit_span;
                     if (bal(l < x && (trg || allc))) break;
                     if (hfa != fa || hfb != fb) {
                         PH_BEGIN(hb)
@@ -3632,7 +3646,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
         const int lk = lower ? 63 - __clzll(lower) : 0;
         const int dsh = shf(dj, lk);
         const int dlk = lower ? dsh : dprev;  // date at position b - 1 when step l starts
-        const bool trig = valid && ((double)dlk - (double)da) >= 1.33 * fit_span;
+        const bool trig = valid && ((double)dlk - (double)da) >= 1.33 * (double)fit_span;
         const unsigned long long TG = bal(trig);
         const unsigned long long Tm = bal(valid && (trig || allc));
         const int nv = popc(V);
@@ -3675,7 +3689,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
             nc = num_coefs(p, b - a);
             fa = a;
             fb = b;
-            fit_span = (double)CDR(P, b - 1) - (double)CDR(P, a);
+            fit_span = CDRU(P, b - 1) - CDRU(P, a);
             nc_fit = nc;
             fmode = 3;  // the refit runs at the top of the loop
             PH_COUNT(P, 34, 1)
@@ -3683,7 +3697,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
     }
     PH_BEGIN(md)
     const double mag_lane = peek_medians(P, k, moff);
-    emit(P, CDR(P, a), CDR(P, b - 1), CDR(P, peek_start), b - a, change, nc, mag_lane);
+    emit(P, CDRU(P, a), CDRU(P, b - 1), CDRU(P, peek_start), b - a, change, nc, mag_lane);
     PH_END(P, md, 11)
     wa = a;
     wb = b;
@@ -3982,7 +3996,7 @@ __device__ __forceinline__ int px_setup(Px &P, int chip, int pix) {
         const int pd = shf(d, pl);
         const int prevd = lower ? pd : carry;
         const bool keep2 = keep && d != prevd;
-        if (km) carry = shf(d, 63 - __clzll(km));
+        if (km) carry = rdl(d, 63 - __clzll(km));
         const unsigned long long k2 = bal(keep2);
         if (keep2) {
             const int pos = gidx(P, m + below(k2), n, __LINE__);
@@ -4037,7 +4051,7 @@ __device__ __forceinline__ void detect_body() {
     for (;;) {
         unsigned long long job = 0;
         if (l == 0) job = atomicAdd(&A.counters[0], 1ull);
-        job = shf((unsigned long long)job, 0);
+        job = uni(job);  // lane 0's
         if (job >= (unsigned long long)A.total_pix) break;
         // chip of this pixel: binary search of the chips' pixel offsets (wave-uniform)
         int lo = 0, hi = A.n_chips - 1;

@@ -31,9 +31,12 @@ batch = bench.build_batch(cfg, ids)
 res = {}
 for r in range(a.rounds):
     for spec in a.libs:
-        # "lib.so:w4" runs the library's 4-waves/SIMD kernel (CCDGPU_KERNEL, read at context creation)
+        # "lib.so:w3" runs the library's 3-waves/SIMD kernel (CCDGPU_KERNEL, read at context creation)
         path, _, variant = spec.partition(':')
-        os.environ['CCDGPU_KERNEL'] = variant or 'w3'
+        if variant:
+            os.environ['CCDGPU_KERNEL'] = variant
+        else:
+            os.environ.pop('CCDGPU_KERNEL', None)  # the library's default kernel
         ccdgpu._lib = None
         ccdgpu.LIB_PATH = path if os.path.isabs(path) else os.path.join(ROOT, 'lcmap-firebird_amd', path)
         ns = argparse.Namespace(chips=a.chips, contexts=a.contexts, warmup=a.warmup, steps=a.steps, config=a.config, roofline_launches=1)
