@@ -158,8 +158,8 @@ struct Px {
     int32_t *cd;  // compacted dates
     CRow *cr;     // compacted rows: 7 band values + sorted index, one 16-byte load per observation
 #endif
-    GLOBAL_AS double *fs;  // per-slot double scratch [8][n]: Tmask columns / closest-DOY r^2 [n][8]
-    GLOBAL_AS uint16_t *bk;  // per-slot closest-DOY bucket list [n]
+    // (the slot's double scratch -- Tmask columns, bucket records, ring overflow -- and its bucket
+    // list are addressed from the launch arguments where used: PFS, PBK)
     int64_t gpix;
     int nseg;
     int acc_a, acc_b;  // window [acc_a, acc_b) whose raw sums L->S holds (acc_a < 0: none)
@@ -173,7 +173,24 @@ __device__ __forceinline__ GLOBAL_AS unsigned *pmask(const Px &P) {
 }
 // peek residuals of observations 64 .. CCDGPU_MAX_PEEK-1, band-major [band][POVF], after the
 // slot's [8][n] double scratch
-__device__ __forceinline__ GLOBAL_AS double *ring_ovf(const Px &P) { return P.fs + (size_t)8 * ARGS().n_obs_max; }
+// The wave's slot (its workgroup: one wave per workgroup) and the slot's double scratch and
+// bucket list, recomputed at every use from the launch arguments (scalar loads) instead of two
+// 64-bit pointers held in scalar registers for the whole kernel; none is read in the hottest loops
+// (the period rows and dates, PCD / PCR, are: those stay in Px).
+__device__ __forceinline__ size_t slot_no() {
+    int s = (int)__builtin_amdgcn_workgroup_id_x();
+    asm volatile("" : "+s"(s));
+    return (size_t)s;
+}
+__device__ __forceinline__ GLOBAL_AS double *PFS(const Px &) {
+    const CcdDetectArgs &A = ARGS();
+    return as_global(A.s_f64 + slot_no() * CCD_SLOT_F64(A.n_obs_max));
+}
+__device__ __forceinline__ GLOBAL_AS uint16_t *PBK(const Px &) {
+    const CcdDetectArgs &A = ARGS();
+    return as_global(A.s_bk + slot_no() * (size_t)A.n_obs_max);
+}
+__device__ __forceinline__ GLOBAL_AS double *ring_ovf(const Px &P) { return PFS(P) + (size_t)8 * ARGS().n_obs_max; }
 
 // Where the compacted period lives.  CCD_PERIOD_IN_LDS: in the wave's LDS block right after the
 // Lds struct (dates, then rows at a 16-byte aligned offset) -- every period access is a ds_*
@@ -383,6 +400,10 @@ __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlan
 __device__ __forceinline__ unsigned long long uni(unsigned long long v) {
     return ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
            (unsigned)__builtin_amdgcn_readfirstlane((int)v);
+}
+__device__ __forceinline__ double unid(double v) {
+    return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                            __builtin_amdgcn_readfirstlane(__double2loint(v)));
 }
 // value of v in a (wave-uniform) lane, as a scalar
 __device__ __forceinline__ int rdl(int v, int src XL) {
@@ -1253,7 +1274,7 @@ __device__ __forceinline__ void variogram(Px &P) {
     // (band-major u16 [7][n]); the same pass histograms every band's differences below 256 in
     // LDS (u16 counters, 128 words per band, in the row tile) and counts them, so a band whose two
     // middle ranks lie below 256 -- nearly always -- needs no further pass over its differences
-    GLOBAL_AS uint16_t *dv = reinterpret_cast<GLOBAL_AS uint16_t *>(P.fs);
+    GLOBAL_AS uint16_t *dv = reinterpret_cast<GLOBAL_AS uint16_t *>(PFS(P));
     uint32_t *h16w = reinterpret_cast<uint32_t *>(&L->row[0][0]);
     for (int i = l; i < NB * 128; i += W) h16w[i] = 0u;
     wsync();
@@ -1667,6 +1688,10 @@ __device__ __forceinline__ int tmask_reg(Px &P, int a, int b) {
                 tm_solve(Gt, r0, coef);
             }
         }
+        // every lane solved the same system (LDS-broadcast normal equations): the coefficients and
+        // the convergence test below are wave-uniform -- as scalars
+#pragma unroll
+        for (int r = 0; r < 5; ++r) coef[r] = unid(coef[r]);
         stat_uniform(ST_FLOPS, (unsigned long long)nw * 35 + 125);  // OLS fit: n_w 35 + 5^3
         int iteration = 1;
         bool converged = false;
@@ -1691,6 +1716,8 @@ __device__ __forceinline__ int tmask_reg(Px &P, int a, int b) {
             tm_normal_reg(x, in ? wt : 0.0, yv, nw, ncol);
             tm_load(L, Gw, rw);
             tm_solve(Gw, rw, coef);
+#pragma unroll
+            for (int r = 0; r < 5; ++r) coef[r] = unid(coef[r]);
             stat_uniform(ST_FLOPS, (unsigned long long)nw * 35 + 125);  // each IRLS refit: n_w 35 + 5^3
             iteration += 1;
             converged = true;
@@ -1711,7 +1738,7 @@ __device__ __forceinline__ int tmask_reg(Px &P, int a, int b) {
     for (int i = l; i < (nw + 31) / 32; i += W) cnt += __popc(L->tflag[i]);
     for (int o = 32; o > 0; o >>= 1) cnt += shfx(cnt, o);
     wsync();
-    return cnt;
+    return uni(cnt);
 }
 
 // ---- Tmask of the two default Tmask bands at once, for windows of at most 32 observations (the
@@ -1951,8 +1978,8 @@ __device__ __forceinline__ int tmask(Px &P, int a, int b) {
     const double w = 2.0 * M_PI / p.avg_days_yr;
     const double oc = w / ceil(((double)CDR(P, b - 1) - (double)CDR(P, a)) / p.avg_days_yr);
     const int ncol = (oc == w) ? 3 : 5;
-    GLOBAL_AS double *xoc = P.fs, *xos = P.fs + P.n, *adj = P.fs + 2 * P.n, *absr = P.fs + 3 * P.n,
-           *wt = P.fs + 4 * P.n;
+    GLOBAL_AS double *xoc = PFS(P), *xos = PFS(P) + P.n, *adj = PFS(P) + 2 * P.n, *absr = PFS(P) + 3 * P.n,
+           *wt = PFS(P) + 4 * P.n;
     if (ncol == 5) tm_trig(P, a, nw, oc, xoc, xos);
     for (int i = l; i < (nw + 31) / 32; i += W) L->tflag[i] = 0u;
     gsync();
@@ -2016,6 +2043,10 @@ __device__ __forceinline__ int tmask(Px &P, int a, int b) {
                 tm_solve(Gt, r0, coef);
             }
         }
+        // every lane solved the same system (LDS-broadcast normal equations): the coefficients and
+        // the convergence test below are wave-uniform -- as scalars
+#pragma unroll
+        for (int r = 0; r < 5; ++r) coef[r] = unid(coef[r]);
         stat_uniform(ST_FLOPS, (unsigned long long)nw * 35 + 125);  // OLS fit: n_w 35 + 5^3
         int iteration = 1;
         bool converged = false;
@@ -2055,6 +2086,8 @@ __device__ __forceinline__ int tmask(Px &P, int a, int b) {
             tm_normal(P, a, nw, ncol, xoc, xos, band, wt);
             tm_load(&LDS(), Gw, rw);
             tm_solve(Gw, rw, coef);
+#pragma unroll
+            for (int r = 0; r < 5; ++r) coef[r] = unid(coef[r]);
             stat_uniform(ST_FLOPS, (unsigned long long)nw * 35 + 125);  // each IRLS refit: n_w 35 + 5^3
             iteration += 1;
             converged = true;
@@ -2082,7 +2115,7 @@ __device__ __forceinline__ int tmask(Px &P, int a, int b) {
     for (int i = l; i < (nw + 31) / 32; i += W) cnt += __popc(L->tflag[i]);
     for (int o = 32; o > 0; o >>= 1) cnt += shfx(cnt, o);
     wsync();
-    return cnt;
+    return uni(cnt);
 }
 
 __device__ __forceinline__ bool tflag_at(const Lds *L, int i) { return (L->tflag[i >> 5] >> (i & 31)) & 1u; }
@@ -2108,7 +2141,7 @@ __device__ __forceinline__ bool stable(const Px &P, int a, int b) {
         const double v = (fabs(slope) + fabs(resid_at(P, l, a)) + fabs(resid_at(P, l, b - 1))) / rn;
         v2 = v * v;
     }
-    return sqrt(wsum(v2)) < LDS().chg;
+    return uni(sqrt(wsum(v2)) < LDS().chg ? 1 : 0) != 0;
 }
 __device__ __forceinline__ void count_stable(Px &P) {}
 
@@ -2201,7 +2234,7 @@ __device__ __forceinline__ bool eval_peek(Px &P, int k, int start, int dir, doub
         const double v = r / rm;
         const double mag = gsum8((valid && det) ? v * v : 0.0);
         if (bal(bnd == 0 && jj < k && !(mag > L->chg))) all = false;
-        if (pass == 0) mag0 = shf(mag, 0);
+        if (pass == 0) mag0 = unid(mag);  // lane 0's: observation 0 (full EXEC here)
     }
     stat_uniform(ST_FLOPS, (unsigned long long)k * (7 * 2 * 8 + 5 * 3));
     PH_COUNT(P, 18, 1)  // predict 7*2*8 + magnitude 5*3 per peek obs
@@ -2406,9 +2439,9 @@ __device__ __forceinline__ void build_closest(const Px &P, int fa, int fb, int k
             const int ub = u1461(dt[u]);
             const unsigned old = atomicAdd(&L->hist2[ub >> 1], 1u << ((ub & 1) * 16));
             const int pos = gidx(P, (int)((old >> ((ub & 1) * 16)) & 0xFFFFu), nf, __LINE__);
-            P.bk[pos] = (uint16_t)(i - fa);
+            PBK(P)[pos] = (uint16_t)(i - fa);
             const unsigned qw[4] = {q.x, q.y, q.z, q.w};
-            GLOBAL_AS double *o = P.fs + (size_t)pos * fw;
+            GLOBAL_AS double *o = PFS(P) + (size_t)pos * fw;
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
                 const double *c = Lc->coef[b];
@@ -2503,7 +2536,7 @@ __device__ __forceinline__ void build_buckets(const Px &P, int fa, int fb) {
             if (i < fb) {
                 const int ub = u1461(dt[u]);
                 const unsigned old = atomicAdd(&L->hist2[ub >> 1], 1u << ((ub & 1) * 16));
-                rec_store(P.fs, gidx(P, (int)((old >> ((ub & 1) * 16)) & 0xFFFFu), nf, __LINE__), q[u]);
+                rec_store(PFS(P), gidx(P, (int)((old >> ((ub & 1) * 16)) & 0xFFFFu), nf, __LINE__), q[u]);
             }
         }
     }
@@ -2678,7 +2711,7 @@ __device__ __forceinline__ void coop_comp(const Px &P, int nf, int dref, const i
             pos = te < c1 ? st1 + te : st2 + (te - c1);
         }
         uint4 q = uint4{0u, 0u, 0u, 0u};
-        if (e < E) q = rec_load(P.fs, gidx(P, pos, nf, __LINE__));
+        if (e < E) q = rec_load(PFS(P), gidx(P, pos, nf, __LINE__));
         const int ci = (int)(q.w >> 16);
         bool take = e < E;
         if (T > need) {
@@ -2690,7 +2723,7 @@ __device__ __forceinline__ void coop_comp(const Px &P, int nf, int dref, const i
             } else {
                 for (int f = 0; f < T; ++f) {
                     const int fp = f < c1 ? st1 + f : st2 + (f - c1);
-                    rank += (int)(rec_load(P.fs, gidx(P, fp, nf, __LINE__)).w >> 16) < ci ? 1 : 0;
+                    rank += (int)(rec_load(PFS(P), gidx(P, fp, nf, __LINE__)).w >> 16) < ci ? 1 : 0;
                 }
             }
             if (tie) take = rank < need;
@@ -2941,8 +2974,8 @@ __device__ __forceinline__ void comp_lane(Px &P, int nf, int dref, double (&cs)[
     const int s0w = gidx(P, s0 >= nf ? s0 - nf : s0, nf, __LINE__);  // bucket position of row 0
     const int lr = less < nf ? less : nf;
     const int n1 = lr < nf - s0w ? lr : nf - s0w;
-    run_add<FW>(P.fs + (size_t)s0w * FW, n1, cs);
-    run_add<FW>(P.fs, lr - n1, cs);
+    run_add<FW>(PFS(P) + (size_t)s0w * FW, n1, cs);
+    run_add<FW>(PFS(P), lr - n1, cs);
     PH_END(P, c2, 22)
     PH_BEGIN(c3)
     const int b1 = (u - K + 1461) % 1461, b2 = (u + K) % 1461;
@@ -2972,7 +3005,7 @@ __device__ __forceinline__ void comp_lane(Px &P, int nf, int dref, double (&cs)[
 #pragma unroll
         for (int e = 0; e < TU; ++e) {
             iv[e] = 0x7FFFFFFF;
-            if (rk && e < Tb) iv[e] = (!all_k && e < T) ? (int)P.bk[pe[e]] : 0x7FFFFFFF;
+            if (rk && e < Tb) iv[e] = (!all_k && e < T) ? (int)PBK(P)[pe[e]] : 0x7FFFFFFF;
         }
         double ws[TU];
 #pragma unroll
@@ -2992,7 +3025,7 @@ __device__ __forceinline__ void comp_lane(Px &P, int nf, int dref, double (&cs)[
                 double f[2][FW];
 #pragma unroll
                 for (int u = 0; u < 2; ++u) {
-                    const GLOBAL_AS double *fp = P.fs + (size_t)pe[e0 + u] * FW;
+                    const GLOBAL_AS double *fp = PFS(P) + (size_t)pe[e0 + u] * FW;
 #pragma unroll
                     for (int bd = 0; bd < FW; ++bd) f[u][bd] = fp[bd];
                 }
@@ -3007,19 +3040,19 @@ __device__ __forceinline__ void comp_lane(Px &P, int nf, int dref, double (&cs)[
     for (int e = 0; e < (T <= TU ? 0 : T); ++e) {
         const int pe = e < c1 ? st1 + e : st2 + (e - c1);
         if (all_k) {
-            const GLOBAL_AS double *f = P.fs + (size_t)gidx(P, pe, nf, __LINE__) * FW;
+            const GLOBAL_AS double *f = PFS(P) + (size_t)gidx(P, pe, nf, __LINE__) * FW;
 #pragma unroll
             for (int bd = 0; bd < FW; ++bd) cs[bd] += f[bd];
             continue;
         }
-        const int ie = (int)P.bk[gidx(P, pe, P.n, __LINE__)];
+        const int ie = (int)PBK(P)[gidx(P, pe, P.n, __LINE__)];
         int rank = 0;
         for (int f2 = 0; f2 < T; ++f2) {
             const int pf = f2 < c1 ? st1 + f2 : st2 + (f2 - c1);
-            rank += ((int)P.bk[gidx(P, pf, P.n, __LINE__)] < ie) ? 1 : 0;
+            rank += ((int)PBK(P)[gidx(P, pf, P.n, __LINE__)] < ie) ? 1 : 0;
         }
         if (rank < need) {
-            const GLOBAL_AS double *f = P.fs + (size_t)gidx(P, pe, nf, __LINE__) * FW;
+            const GLOBAL_AS double *f = PFS(P) + (size_t)gidx(P, pe, nf, __LINE__) * FW;
 #pragma unroll
             for (int bd = 0; bd < FW; ++bd) cs[bd] += f[bd];
         }
@@ -4038,8 +4071,6 @@ __device__ __forceinline__ void detect_body() {
     P.cd = A.s_date + (size_t)slot * nmax;
     P.cr = reinterpret_cast<CRow *>(A.s_row) + (size_t)slot * nmax;
 #endif
-    P.fs = as_global(A.s_f64 + (size_t)slot * CCD_SLOT_F64(nmax));
-    P.bk = as_global(A.s_bk + (size_t)slot * nmax);
     P.bad = 0;
     if (l < 4) lds.stat[l] = 0ull;
 #ifdef CCD_PHASE_TIMERS
@@ -4077,8 +4108,8 @@ __device__ __forceinline__ void detect_body() {
             uint4 *w = reinterpret_cast<uint4 *>(&lds);
             for (int i = l; i < (int)(offsetof(Lds, stat) / 16); i += W) w[i] = uint4{~0u, ~0u, ~0u, ~0u};
             // ... nor from the slot's global scratch
-            for (size_t i = l; i < CCD_SLOT_F64(nmax); i += W) P.fs[i] = __longlong_as_double(-1ll);
-            for (size_t i = l; i < nmax; i += W) P.bk[i] = 0xFFFFu;
+            for (size_t i = l; i < CCD_SLOT_F64(nmax); i += W) PFS(P)[i] = __longlong_as_double(-1ll);
+            for (size_t i = l; i < nmax; i += W) PBK(P)[i] = 0xFFFFu;
 #ifndef CCD_PERIOD_IN_LDS
             for (size_t i = l; i < nmax; i += W) {
                 P.cd[i] = -1;
