@@ -65,6 +65,11 @@ typedef struct ccdgpu_params {
     double lasso_tol;           /* 1e-4                                                  */
     double clear_pct_threshold; /* 0.25                                                  */
     double snow_pct_threshold;  /* 0.75                                                  */
+    /* tie order of the date sort (ccd/__init__.py detect) and of find_closest_doy
+       (change.py): 0 = numpy's argsort kind='quicksort' as the pinned reference image ran it
+       (numpy < 1.17 introsort-free aquicksort), 1 = stable (ties by position) */
+    int32_t argsort_stable;     /* 0                                                     */
+    int32_t reserved0;          /* 0                                                     */
 } ccdgpu_params;
 
 /* One change model (pyccd change_model dict; ccdc/pyccd.py:106-148 formats it). */

@@ -34,6 +34,7 @@ class Params(ctypes.Structure):
         ('avg_days_yr', _f64), ('change_probability', _f64), ('change_threshold', _f64),
         ('outlier_threshold', _f64), ('t_const', _f64), ('lasso_alpha', _f64),
         ('lasso_tol', _f64), ('clear_pct_threshold', _f64), ('snow_pct_threshold', _f64),
+        ('argsort_stable', _i32), ('reserved0', _i32),
     ]
 
 
@@ -171,6 +172,7 @@ def default_params():
     p.change_threshold, p.outlier_threshold = 15.086272469388987, 35.888186879610423
     p.t_const, p.lasso_alpha, p.lasso_tol = 4.42, 1.0, 1e-4
     p.clear_pct_threshold, p.snow_pct_threshold = 0.25, 0.75
+    p.argsort_stable = 0  # numpy quicksort tie order (the pinned reference's)
     return p
 
 
@@ -191,6 +193,10 @@ def params_from_dict(d=None):
             p.curve_qa_end = v.get('END', p.curve_qa_end)
             p.curve_qa_insuf_clear = v.get('INSUF_CLEAR', p.curve_qa_insuf_clear)
             p.curve_qa_persist_snow = v.get('PERSIST_SNOW', p.curve_qa_persist_snow)
+        elif k == 'ARGSORT':
+            if v not in ('quicksort', 'stable'):
+                raise ValueError("ARGSORT must be 'quicksort' or 'stable', not %r" % (v,))
+            p.argsort_stable = 1 if v == 'stable' else 0
         elif k in ('FITTER_FN',):
             pass
         else:

@@ -82,13 +82,12 @@ extern "C" {
 #endif
 // kernel launchers (ccd_kernels.hip)
 int ccdk_prep(const int64_t *dates, int32_t n_chips, const int32_t *chip_nobs, const int64_t *chip_obs_off,
-              double avg_days_yr, int32_t *order, int64_t *sdates, double *basis, void *stream);
+              double avg_days_yr, int32_t argsort_stable, int32_t *order, int64_t *sdates, double *basis,
+              void *stream);
 // the detection kernel reads its arguments from slot arg_slot of a __constant__ array (one slot
 // per live context, so contexts on one device may launch concurrently from their own streams)
 int ccdk_set_args(const CcdDetectArgs *host_args, int arg_slot, void *stream);
 int ccdk_detect(int32_t grid, int variant, int32_t n_obs_max, int arg_slot, void *stream);
-// 1 if this build keeps the compacted period in LDS (-DCCD_PERIOD_IN_LDS)
-int ccdk_period_in_lds(void);
 // dynamic LDS bytes per wave and resident waves per CU for a period of n_obs observations
 size_t ccdk_lds_bytes(int32_t n_obs);
 int ccdk_occupancy(int variant, int32_t n_obs);

@@ -77,7 +77,7 @@ struct __attribute__((aligned(16))) Lds {
     double comp[8];        // comparison rmse per band (change_magnitude)
     double med1[8], med2[8];
     double chg;            // change threshold of the pixel's (adaptive) peek (change.py)
-    int sel[32];           // compacted indices of the 24 closest-DOY observations
+    int sel[32];           // qs_ties: pending parts of the replayed quicksort
 #ifdef CCD_PHASE_TIMERS
     unsigned long long tph[CCD_NPHASE];  // diagnostic build: per-phase cycle totals of this wave
 #endif
@@ -154,10 +154,8 @@ struct Px {
     int peek;   // (adaptive) peek size
     const GLOBAL_AS double *basis;
     const int64_t *sd;
-#ifndef CCD_PERIOD_IN_LDS
     int32_t *cd;  // compacted dates
     CRow *cr;     // compacted rows: 7 band values + sorted index, one 16-byte load per observation
-#endif
     // (the slot's double scratch -- Tmask columns, bucket records, ring overflow -- and its bucket
     // list are addressed from the launch arguments where used: PFS, PBK)
     int64_t gpix;
@@ -192,20 +190,10 @@ __device__ __forceinline__ GLOBAL_AS uint16_t *PBK(const Px &) {
 }
 __device__ __forceinline__ GLOBAL_AS double *ring_ovf(const Px &P) { return PFS(P) + (size_t)8 * ARGS().n_obs_max; }
 
-// Where the compacted period lives.  CCD_PERIOD_IN_LDS: in the wave's LDS block right after the
-// Lds struct (dates, then rows at a 16-byte aligned offset) -- every period access is a ds_*
-// instruction; otherwise in the per-slot global scratch.
-#ifdef CCD_PERIOD_IN_LDS
-__device__ __forceinline__ int cd_bytes(int n) { return (4 * n + 15) & ~15; }
-__device__ __forceinline__ int32_t *PCD(const Px &) { return reinterpret_cast<int32_t *>(ccd_smem + sizeof(Lds)); }
-__device__ __forceinline__ CRow *PCR(const Px &P) {
-    return reinterpret_cast<CRow *>(ccd_smem + sizeof(Lds) + cd_bytes(P.n));
-}
-#else
+// The compacted period lives in the per-slot global scratch (round 2 measured it in LDS: one wave
+// per SIMD, slower).
 __device__ __forceinline__ int32_t *PCD(const Px &P) { return P.cd; }
 __device__ __forceinline__ CRow *PCR(const Px &P) { return P.cr; }
-#endif
-static_assert(sizeof(Lds) % 16 == 0, "period rows follow the Lds block 16-byte aligned");
 
 // ------------------------------------------------------------------ diagnostic phase timers
 // Built only into lib/libccdgpu_diag.so (-DCCD_PHASE_TIMERS): s_memtime cycle totals per phase,
@@ -264,13 +252,8 @@ __device__ __forceinline__ int gidx(const Px &P, int j, int lim, int line) {
 #endif
 }
 // physical row of logical row j (gap buffer)
-// (-DCCD_NO_GAP: no gap buffer -- a removal shifts the whole tail, rows never move otherwise)
 __device__ __forceinline__ int ph(const Px &P, int j) {
-#ifdef CCD_NO_GAP
-    return j;
-#else
     return j + (j >= P.gp ? P.gl : 0);
-#endif
 }
 // guarded logical row -> physical row
 __device__ __forceinline__ int prow(const Px &P, int j, int line) { return ph(P, gidx(P, j, P.m, line)); }
@@ -430,11 +413,7 @@ __device__ __forceinline__ void wsync() {
 }
 __device__ __forceinline__ void gsync() { __syncthreads(); }
 // psync: hand-off of compacted-period data written by one lane and read by another
-#ifdef CCD_PERIOD_IN_LDS
-__device__ __forceinline__ void psync() { wsync(); }
-#else
 __device__ __forceinline__ void psync() { gsync(); }
-#endif
 
 #define cvalf(P, b, j) ((double)CVR(P, b, j))
 
@@ -552,13 +531,9 @@ __device__ __forceinline__ int compact_drop(Px &P, int lo, int hi, F drop) {
     const int l = lane();
     if (lo < P.acc_b) P.acc_a = -1;  // rows of the accumulated Gram window may move
     hi = hi < P.m ? hi : P.m;
-#ifdef CCD_NO_GAP
-    const int a = lo, e = P.m;
-#else
     if (P.gl == 0) P.gp = lo;  // an empty gap moves for free: start it at the first removal
     const int a = lo < P.gp ? lo : P.gp;
     const int e = hi > P.gp ? hi : (P.gp < P.m ? P.gp : P.m);
-#endif
     PH_COUNT(P, 31, e - a)
     int out = a;
     // four 64-row chunks per round: all their loads go out before the first store (a row's
@@ -599,10 +574,8 @@ __device__ __forceinline__ int compact_drop(Px &P, int lo, int hi, F drop) {
     }
     const int removed = (e - a) - (out - a);
     P.m -= removed;
-#ifndef CCD_NO_GAP
     P.gl += removed;
     P.gp = out;
-#endif
     psync();
     return P.m;
 }
@@ -989,13 +962,7 @@ __device__ __forceinline__ int cd_sweep(Lds *L, int pc_rt, double alpha, int max
     return sweeps;
 }
 // the sweep with its coordinate count unrolled for the three model sizes (no per-coordinate branch)
-// (-DCCD_CD_CALL: one out-of-line copy shared by every fit_models call site instead of one inlined
-// copy per site -- fewer instruction-cache lines for the waves to share, a call's register saves)
-#ifdef CCD_CD_CALL
-__device__ __attribute__((noinline)) int cd_lanes(Lds *L, int pc, double alpha, int max_iter, double tol) {
-#else
 __device__ __forceinline__ int cd_lanes(Lds *L, int pc, double alpha, int max_iter, double tol) {
-#endif
     switch (pc) {
     case 3: return cd_sweep<3>(L, pc, alpha, max_iter, tol);
     case 5: return cd_sweep<5>(L, pc, alpha, max_iter, tol);
@@ -1018,7 +985,7 @@ __device__ __forceinline__ double resid_at(const Px &P, int band, int j) {
 }
 
 // lasso.fitted_model for the 7 bands over compacted window [a, b) with k coefficients.
-// with_rmse = false leaves L->rmse to the caller (build_closest computes it from the same
+// with_rmse = false leaves L->rmse to the caller (fit_bounds computes it from the same
 // residuals).  A window and k equal to the last fit's keep the models as they are.
 __device__ __forceinline__ void fit_models(Px &P, int a, int b, int k, bool with_rmse = true) {
     const ccdgpu_params &p = ARGS().p;
@@ -1968,12 +1935,10 @@ __device__ __forceinline__ int tmask(Px &P, int a, int b) {
     Lds *L = &LDS();
     const int l = lane();
     const int nw = b - a;
-#ifndef CCD_NO_TMASK_PAIR
     if (nw <= 32 && __builtin_popcount(p.tmask_bands & 0x7Fu) == 2) {
         const int bA = __builtin_ctz(p.tmask_bands), bB = 31 - __builtin_clz(p.tmask_bands & 0x7Fu);
         return tmask_pair(P, a, b, bA, bB);
     }
-#endif
     if (nw <= W) return tmask_reg(P, a, b);
     const double w = 2.0 * M_PI / p.avg_days_yr;
     const double oc = w / ceil(((double)CDR(P, b - 1) - (double)CDR(P, a)) / p.avg_days_yr);
@@ -2308,26 +2273,22 @@ __device__ __forceinline__ void lookback(Px &P, int &wa, int &wb, int prev) {
     wb = b;
 }
 
-// find_closest_doy(period, ref, fit_window, 24) -> comparison rmse sqrt(sum r^2) / 4 per band
-// into L->comp.  The key |round(d / 365.25) * 365.25 - d| of d = t - t_ref is exactly
-// min(r, 1461 - r) / 4 with r = (4 t - 4 t_ref) mod 1461 (verified over all |d| <= 20000), so with
-// u = 4 t mod 1461 the 24 closest observations are the bins within distance K of u_ref plus the
-// lowest-index ones of the two bins at distance exactly K (stable argsort order, the documented
-// tie rule).
+// find_closest_doy(period, ref, fit_window, 24) -> comparison rmse sqrt(sum r^2) / 4 per detection
+// band.  The key |round(d / 365.25) * 365.25 - d| of d = t - t_ref is exactly min(r, 1461 - r) / 4
+// with r = (4 t - 4 t_ref) mod 1461 (verified over all |d| <= 20000), so with u = 4 t mod 1461 the
+// 24 closest observations are the entries of the bins within distance K of u_ref -- K the
+// smallest distance holding 24 -- and, when the two bins at distance exactly K hold more entries
+// than the 24 still need, the ones numpy's argsort puts first (qs_ties below).
 //
-// The fit window and the model only change at a refit, so once per (fit window, model) the window
-// is counting-sorted by u into a bucket list (P.bk, fit-relative indices; L->hist2 keeps the bin
-// end positions) and every observation's squared residuals are stored in bucket order
-// (P.fs[pos * FW + s], s-th detection band).  A lookforward step then needs no pass over the window: the bins closer
-// than K are one circular run of bucket positions, read with one coalesced load per band.
+// Per fit the window is counted into the 1461 bins (L->hist2, bin end positions: fit_bounds), and
+// the comparison rmse is first bounded (comp_bound); only a step the bounds leave open gets the
+// exact value (coop_comp), from bucket records -- the fit window's 16-byte period rows
+// counting-sorted by u (build_buckets) -- so the entries closer than K are one circular run of
+// bucket positions.
 __device__ __forceinline__ int u1461(int t) { return (4 * t) % 1461; }
-// The bucket-ordered squared residuals are kept for the detection bands only (the comparison rmse
-// enters change_magnitude and nothing else): row s of an entry is the s-th detection band, rows
-// are FSW(mask) doubles wide (5 for the default five bands, 7 otherwise; unused rows hold 0).
 __device__ __forceinline__ unsigned det_mask() { return ARGS().p.detection_bands & 0x7Fu; }
-__device__ __forceinline__ int fs_width(unsigned dm) { return __builtin_popcount(dm) <= 5 ? 5 : 7; }
-// L->hist2 holds two u16 per word: plain counts (closest_doy_scan) or, after build_closest, the
-// end position of each bin in the bucket list.
+// L->hist2 holds two u16 per word: plain counts (build_hist) or the end position of each bin in
+// the bucket list (bins_prefix).
 __device__ __forceinline__ int h16(const Lds *L, int u) { return (int)L->hist16[u]; }  // = hist2[u/2] half u%2
 __device__ __forceinline__ int bend(const Lds *L, int u) { return h16(L, u); }
 __device__ __forceinline__ int bstart(const Lds *L, int u) { return u == 0 ? 0 : h16(L, u - 1); }
@@ -2352,118 +2313,6 @@ __device__ __forceinline__ void build_hist(const Px &P, int fa, int fb) {
         }
     }
     wsync();
-}
-
-// Counting sort of the fit window [fa, fb) by u into P.bk and the squared residuals of the
-// current models (L->coef) in bucket order into P.fs.
-__device__ __forceinline__ void build_closest(const Px &P, int fa, int fb, int k) {
-    Lds *L = &LDS();
-    const int l = lane();
-    const int nf = fb - fa;
-    build_hist(P, fa, fb);
-    // exclusive prefix over the 1461 bins: lane l owns words [12 l, 12 l + 12) (24 bins)
-    // (the lane's 12 words read at once: 732 = 61 lanes x 12)
-    unsigned hv[12];
-    const bool hl = l < 61;
-#pragma unroll
-    for (int i = 0; i < 12; ++i) hv[i] = hl ? L->hist2[12 * l + i] : 0u;
-    int tot = 0;
-#pragma unroll
-    for (int i = 0; i < 12; ++i) tot += (int)(hv[i] & 0xFFFFu) + (int)(hv[i] >> 16);
-    int run = wscan_incl(tot) - tot;
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {
-        const int s0 = run;
-        const int s1 = run + (int)(hv[i] & 0xFFFFu);
-        run = s1 + (int)(hv[i] >> 16);
-        if (hl) L->hist2[12 * l + i] = (unsigned)s0 | ((unsigned)s1 << 16);  // bin start positions
-    }
-    wsync();
-    // fill: each add advances the bin's cursor, so afterwards every bin holds its end position.
-    // The same pass writes the observation's squared residuals (current models) at its bucket
-    // position (lane = observation: its row and design loads go out before the LDS atomic);
-    // their sums are the models' rmse (lasso.fitted_model) over the same fit window.
-    const Lds *Lc = L;
-    const unsigned dm = det_mask();
-    const int nd = __builtin_popcount(dm), fw = fs_width(dm);
-    double ssq[NB];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) ssq[b] = 0.0;
-    // Two chunks per round, software-pipelined: the next round's rows and dates load while this
-    // round's design rows load and its entries are filled, so a round exposes one memory round
-    // trip (the design rows, which need the row's sorted index) instead of two.
-    uint4 qn[2];
-    int dn[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        const int i = fa + u * W + l;
-        qn[u] = uint4{0u, 0u, 0u, 0u};
-        dn[u] = 0;
-        if (i < fb) {
-            qn[u] = CROW4(P, i);
-            dn[u] = CDR(P, i);
-        }
-    }
-    for (int i0 = fa; i0 < fb; i0 += 2 * W) {
-        uint4 qv[2];
-        int dt[2];
-        double xv[2][7];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            qv[u] = qn[u];
-            dt[u] = dn[u];
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int i = i0 + u * W + l;
-            const GLOBAL_AS double *bs = P.basis + (size_t)gidx(P, i < fb ? (int)(qv[u].w >> 16) : 0, P.n, __LINE__) * CCD_BASIS_STRIDE;
-#pragma unroll
-            for (int c = 0; c < 7; ++c) xv[u][c] = bs[c];
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int i = i0 + (2 + u) * W + l;
-            qn[u] = uint4{0u, 0u, 0u, 0u};
-            dn[u] = 0;
-            if (i < fb) {
-                qn[u] = CROW4(P, i);
-                dn[u] = CDR(P, i);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int i = i0 + u * W + l;
-            if (i >= fb) continue;
-            const uint4 q = qv[u];
-            const double *x = xv[u];
-            const int ub = u1461(dt[u]);
-            const unsigned old = atomicAdd(&L->hist2[ub >> 1], 1u << ((ub & 1) * 16));
-            const int pos = gidx(P, (int)((old >> ((ub & 1) * 16)) & 0xFFFFu), nf, __LINE__);
-            PBK(P)[pos] = (uint16_t)(i - fa);
-            const unsigned qw[4] = {q.x, q.y, q.z, q.w};
-            GLOBAL_AS double *o = PFS(P) + (size_t)pos * fw;
-#pragma unroll
-            for (int b = 0; b < NB; ++b) {
-                const double *c = Lc->coef[b];
-                double pr = x[0] * c[0];
-#pragma unroll
-                for (int jj = 1; jj < 7; ++jj) pr += x[jj] * c[jj];
-                pr += c[7];
-                const double y = (double)(int16_t)(qw[b >> 1] >> ((b & 1) * 16));
-                const double r = y - pr;
-                if ((dm >> b) & 1u) o[__builtin_popcount(dm & ((1u << b) - 1u))] = r * r;
-                ssq[b] += r * r;
-            }
-            for (int t = nd; t < fw; ++t) o[t] = 0.0;
-        }
-    }
-    const double den = (double)(nf - (ARGS().p.rmse_dof ? k : 0));
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        const double t = wsum(ssq[b]);
-        if (l == b) L->rmse[b] = sqrt(t / den);
-    }
-    gsync();
 }
 
 // 16-byte bucket records in the slot's global scratch (a native vector type: loads and stores
@@ -2543,13 +2392,10 @@ __device__ __forceinline__ void build_buckets(const Px &P, int fa, int fb) {
     gsync();  // the records are read by other lanes
 }
 
-#ifndef CCD_FBU
-#define CCD_FBU 2  // chunks of 64 observations per round of fit_bounds' residual pass
-#endif
 // Per fit (lookforward, more than 24 fit observations), once it is needed: lasso.fitted_model's
-// rmse of the current models over the fit window [fa, fb) -- the same arithmetic, per-lane order
-// and wave reduction as build_closest's (lane l sums observations fa + l, fa + l + 64, ...), so
-// the value is bit-identical to it -- and, from the same residuals, the comparison-rmse bounds of
+// rmse of the current models over the fit window [fa, fb) -- lane l sums observations fa + l,
+// fa + l + 64, ... in order, then one wave sum: the order of round 4's bucket build, so the emitted
+// rmse of these fits is unchanged since then -- and, from the same residuals, the comparison-rmse bounds of
 // the batched steps: the window's bin end positions (L->hist2) and per block of 46 bins the sum
 // of its squared residuals per detection band (L->blk, float, every term rounded up).
 __device__ __forceinline__ void fit_bounds(const Px &P, int fa, int fb, int k) {
@@ -2566,9 +2412,10 @@ __device__ __forceinline__ void fit_bounds(const Px &P, int fa, int fb, int k) {
     double ssq[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) ssq[b] = 0.0;
-    // FU chunks per round, software-pipelined as build_closest: the next round's rows and dates
-    // load while this round's design rows load (lane l still adds fa + l, fa + l + 64, ... in order)
-    constexpr int FU = CCD_FBU;
+    // FU chunks per round, software-pipelined: the next round's rows and dates load while this
+    // round's design rows load (lane l still adds fa + l, fa + l + 64, ... in order); one or three
+    // chunks per round measured slower
+    constexpr int FU = 2;
     uint4 qn[FU];
     int dn[FU];
 #pragma unroll
@@ -2657,15 +2504,174 @@ __device__ __forceinline__ void fit_bounds(const Px &P, int fa, int fb, int k) {
     wsync();
 }
 
+// ---- the reference's argsort tie order at distance K (change.find_closest_doy)
+// np.argsort(d_yr)[:24] with numpy's default quicksort as the pinned reference image ran it (numpy
+// < 1.17 aquicksort, restated and pinned against a real numpy build in oracle/ccd_oracle.c
+// ccdoracle_np_argsort): its tie order decides WHICH of the entries at exactly distance K enter
+// the comparison rmse when the two bins at K hold more entries than the 24 still need.  That
+// order depends on the whole sort, so the wave replays it on the fit window's keys -- element
+// key << 12 | sorted index in fit-window order (the order np.argsort sees), in the slot's scratch
+// after the bucket records -- partitioning only the parts that overlap positions [less, 24), the
+// ones whose content is wanted (parts are disjoint ranges permuted within themselves, so the
+// others do not matter).  A partition (median of three parked at pr - 1, Sedgewick's scans that
+// stop on keys equal to the pivot) is computed in parallel: with S the positions in (pl, pr - 1]
+// whose key is >= the pivot (ascending, s_k) and T those in [pl, pr - 2] whose key is <= it
+// (descending, t_k), the sequential scans swap s_k <-> t_k for every k with s_k < t_k (a prefix
+// of k: K1 pairs) and stop at pi = min(s_{K1+1}, t_{K1}) -- the scans only ever meet untouched
+// positions before that -- then pi <-> pr - 1.  Parts of <= 16 entries are insertion-sorted
+// (= stably by key).  Returns in lane j < 24 - less the sorted index of the entry numpy puts at
+// position less + j (the taken ties), -1 elsewhere.  Only steps whose exact comparison rmse is
+// needed AND whose ties straddle the 24th position get here.
+__device__ __forceinline__ unsigned qkey(unsigned x) { return x >> 12; }
+__device__ __forceinline__ int qs_ties(const Px &P, int fa, int nf, int dref, int less) {
+    Lds *L = &LDS();
+    const int l = lane();
+    GLOBAL_AS uint32_t *A = reinterpret_cast<GLOBAL_AS uint32_t *>(PFS(P) + 2 * (size_t)P.n);
+    GLOBAL_AS uint16_t *MS = reinterpret_cast<GLOBAL_AS uint16_t *>(A + P.n);  // s_k by k - 1
+    const int ur = u1461(dref);
+    for (int i0 = 0; i0 < nf; i0 += W) {
+        const int i = i0 + l;
+        if (i < nf) {
+            int r = u1461(CDR(P, fa + i)) - ur;
+            r += r < 0 ? 1461 : 0;
+            const int key = r < 1461 - r ? r : 1461 - r;
+            A[i] = ((unsigned)key << 12) | (unsigned)CIR(P, fa + i);
+        }
+    }
+    gsync();
+    const int lo = less, hi = 24;  // positions whose content is wanted
+    int sp = 0;                    // pending parts: L->sel as pl | pr << 16
+    int pl = 0, pr = nf - 1;
+    for (;;) {
+        while (pr - pl > 15) {
+            const int pm = pl + ((pr - pl) >> 1);
+            unsigned a0 = (unsigned)uni((int)A[pl]), am = (unsigned)uni((int)A[pm]);
+            unsigned ar = (unsigned)uni((int)A[pr]);
+            const unsigned ap = (unsigned)uni((int)A[pr - 1]);
+            unsigned t;
+            if (qkey(am) < qkey(a0)) { t = am; am = a0; a0 = t; }
+            if (qkey(ar) < qkey(am)) { t = ar; ar = am; am = t; }
+            if (qkey(am) < qkey(a0)) { t = am; am = a0; a0 = t; }
+            const unsigned vp = qkey(am);
+            if (l == 0) {  // median of three in place, the pivot parked at pr - 1
+                A[pl] = a0;
+                A[pr] = ar;
+                A[pm] = ap;
+                A[pr - 1] = am;
+            }
+            gsync();
+            int nT = 0;  // T: positions in [pl, pr - 2] with key <= pivot
+            for (int p0 = pl; p0 <= pr - 2; p0 += W) {
+                const int q = p0 + l;
+                const bool in = q <= pr - 2 && qkey(A[q]) <= vp;
+                nT += popc(bal(in));
+            }
+            // S ascending: s_k (k = rank) swaps with t_k while t_k > s_k, i.e. while more than
+            // k - 1 positions of T lie past s_k; the first S position failing that is s_{K1+1}
+            int cS = 0, cT = 0, K1 = -1, sfail = pr - 1;
+            for (int p0 = pl; p0 <= pr - 1 && K1 < 0; p0 += W) {
+                const int q = p0 + l;
+                const unsigned x = q <= pr - 1 ? A[q] : 0u;
+                const unsigned kx = qkey(x);
+                const bool inS = q >= pl + 1 && q <= pr - 1 && kx >= vp;
+                const bool inT = q <= pr - 2 && kx <= vp;
+                const unsigned long long bS = bal(inS), bT = bal(inT);
+                const int rs = cS + below(bS) + 1;
+                const int tgt = nT - (cT + below(bT) + (inT ? 1 : 0));  // T positions past q
+                const bool ok = inS && tgt >= rs;
+                if (ok) MS[gidx(P, rs - 1, P.n, __LINE__)] = (uint16_t)q;
+                const unsigned long long bF = bal(inS && !ok);
+                if (bF) {
+                    const int f = __ffsll((long long)bF) - 1;
+                    sfail = p0 + f;
+                    K1 = rdl(rs, f) - 1;
+                }
+                cS += popc(bS);
+                cT += popc(bT);
+            }
+            K1 = K1 < 0 ? 0 : K1;  // (pr - 1 holds the pivot: it always fails)
+            // T descending: t_k (k = rank from the right) <-> s_k for k <= K1
+            int tK = pr - 1;
+            if (K1 > 0) {
+                gsync();  // MS
+                int cR = 0;
+                for (int p1 = pr - 2; p1 >= pl && cR < K1; p1 -= W) {
+                    const int q = p1 - l;  // lane 0 rightmost
+                    const unsigned x = q >= pl ? A[q] : 0u;
+                    const bool inT = q >= pl && qkey(x) <= vp;
+                    const unsigned long long bT = bal(inT);
+                    const int rt = cR + below(bT) + 1;
+                    if (inT && rt <= K1) {
+                        const int sq = gidx(P, (int)MS[gidx(P, rt - 1, P.n, __LINE__)], nf, __LINE__);
+                        const unsigned xs = A[sq];
+                        A[sq] = x;
+                        A[q] = xs;
+                    }
+                    const unsigned long long bK = bal(inT && rt == K1);
+                    if (bK) tK = p1 - (__ffsll((long long)bK) - 1);
+                    cR += popc(bT);
+                }
+            }
+            gsync();
+            const int pi = K1 > 0 && tK < sfail ? tK : sfail;
+            {
+                const unsigned xpi = (unsigned)uni((int)A[pi]), xp1 = (unsigned)uni((int)A[pr - 1]);
+                if (l == 0) {
+                    A[pi] = xp1;
+                    A[pr - 1] = xpi;
+                }
+                gsync();
+            }
+            // the parts that overlap [lo, hi): continue with one, keep the other
+            const bool rl = pl < hi && pi - 1 >= lo && pi - 1 >= pl;
+            const bool rr = pi + 1 < hi && pr >= lo && pr >= pi + 1;
+            if (rl && rr) {
+                if (l == 0) L->sel[sp < 31 ? sp : 31] = (pi + 1) | (pr << 16);
+                sp += 1;
+                pr = pi - 1;
+            } else if (rl) {
+                pr = pi - 1;
+            } else if (rr) {
+                pl = pi + 1;
+            } else {
+                pl = 1;
+                pr = 0;
+                break;
+            }
+        }
+        if (pr >= pl) {  // insertion sort of a part of <= 16 entries: stable by key
+            const int cnt = pr - pl + 1;
+            const unsigned x = l < cnt ? A[pl + l] : 0xFFFFFFFFu;
+            const unsigned kx = qkey(x);
+            int pos = 0;
+            for (int j = 0; j < cnt; ++j) {
+                const unsigned kj = qkey((unsigned)rdl((int)x, j));
+                pos += (kj < kx || (kj == kx && j < l)) ? 1 : 0;
+            }
+            if (l < cnt) A[pl + pos] = x;
+            gsync();
+        }
+        if (sp == 0) break;
+        sp -= 1;
+        wsync();
+        const int e = uni(L->sel[sp < 31 ? sp : 31]);
+        pl = e & 0xFFFF;
+        pr = e >> 16;
+    }
+    const int need = hi - lo;
+    return l < need ? (int)(A[lo + l] & 0xFFFu) : -1;
+}
+
 // find_closest_doy comparison rmse of ONE batched step (reference date dref) from the bucket
 // records, the whole wave working on it: the distance K of the 24th closest entry by a scan over
-// the bin ends (as closest_doy_scan), then lane = entry -- the circular run of bucket positions
-// closer than K and the entries at exactly K (the lowest sorted indices of those taken: the
-// stable argsort's tie rule; sorted index order is fit-window order) -- each taken lane
-// recomputes its residuals of the detection bands from its record and design row (resid_at's
-// arithmetic) and the squares are summed over the wave.  Returns sqrt(sum) / 4 of the s-th
-// detection band in out[s] (every lane).  nf > 24.
-__device__ __forceinline__ void coop_comp(const Px &P, int nf, int dref, const int (&bs)[NB], int nd,
+// the bin ends, then lane = entry -- the circular run of bucket positions
+// closer than K and the entries at exactly K (when more are there than needed: the ones numpy's
+// quicksort puts first, qs_ties; with argsort_stable the lowest sorted indices -- sorted index
+// order is fit-window order) -- each taken lane recomputes its residuals of the detection bands
+// from its record and design row (resid_at's arithmetic) and the squares are summed over the
+// wave.  Returns sqrt(sum) / 4 of the s-th detection band in out[s] (every lane).  Fit window
+// [fa, fa + nf), nf > 24.
+__device__ __forceinline__ void coop_comp(const Px &P, int fa, int nf, int dref, const int (&bs)[NB], int nd,
                                           double (&out)[NB]) {
     const unsigned dm = det_mask();
     const Lds *L = &LDS();
@@ -2696,6 +2702,9 @@ __device__ __forceinline__ void coop_comp(const Px &P, int nf, int dref, const i
     const int c1 = bcount(L, b1), c2 = K > 0 ? bcount(L, b2) : 0;
     const int st1 = bstart(L, b1), st2 = bstart(L, b2);
     const int T = c1 + c2, E = less + T;
+    // numpy's choice among the ties (lane j < need: the sorted index of the j-th one taken)
+    const bool qs = T > need && !ARGS().p.argsort_stable;
+    const int tk = qs ? qs_ties(P, fa, nf, dref, less) : -1;
     double acc[NB];  // per band (detection bands only)
 #pragma unroll
     for (int b = 0; b < NB; ++b) acc[b] = 0.0;
@@ -2714,9 +2723,18 @@ __device__ __forceinline__ void coop_comp(const Px &P, int nf, int dref, const i
         if (e < E) q = rec_load(PFS(P), gidx(P, pos, nf, __LINE__));
         const int ci = (int)(q.w >> 16);
         bool take = e < E;
-        if (T > need) {
-            // more entries at distance K than needed: a tie entry is taken when fewer than
-            // `need` of them have a smaller sorted index
+        if (qs) {
+            // more entries at distance K than needed: a tie entry is taken when numpy's argsort
+            // puts it among the first 24
+            bool in = false;
+            for (int j = 0; j < need; ++j) {
+                const int cj = rdl(tk, j);  // (full EXEC: no short-circuit around the readlane)
+                in = in | (cj == ci);
+            }
+            if (tie) take = in;
+        } else if (T > need) {
+            // (argsort_stable) a tie entry is taken when fewer than `need` of them have a
+            // smaller sorted index
             int rank = 0;
             if (E <= W) {
                 for (int f = 0; f < T; ++f) rank += rdl(ci, less + f) < ci ? 1 : 0;
@@ -2761,55 +2779,20 @@ __device__ __forceinline__ void coop_comp(const Px &P, int nf, int dref, const i
     }
 }
 
-__device__ __forceinline__ void closest_doy_scan(Px &P, int fa, int fb, int ref_idx) {
+// comparison rmse of a fit window of <= 24 observations (all of them: find_closest_doy(...)[:24]
+// takes every one) into L->comp, for every band
+__device__ __forceinline__ void closest_doy_scan(Px &P, int fa, int fb) {
     Lds *L = &LDS();
     const int l = lane();
-    const int nf = fb - fa;
-    const int ur = u1461(CDR(P, ref_idx));
-    int K = 1 << 20, need = 0;
-    if (nf > 24) {
-        int carry = 0;
-        for (int base = 0; base <= 730; base += W) {
-            const int dd = base + l;
-            int c = 0;
-            if (dd == 0) c = bcount(L, ur);
-            else if (dd <= 730) c = bcount(L, (ur + dd) % 1461) + bcount(L, (ur - dd + 1461) % 1461);
-            const int cum = wscan_incl(c) + carry;
-            const unsigned long long hit = bal(cum >= 24);
-            if (hit) {
-                const int src = __ffsll((long long)hit) - 1;
-                K = base + src;
-                need = 24 - (rdl(cum, src) - rdl(c, src));
-                break;
-            }
-            carry = rdl(cum, W - 1);
-        }
-    }
-    int taken_eq = 0, nsel = 0;
-    for (int t0 = 0; t0 < nf; t0 += W) {
-        const int i = t0 + l;
-        int kv = 1 << 21;
-        if (i < nf) {
-            int r = u1461(CDR(P, fa + i)) - ur;
-            r = r < 0 ? r + 1461 : r;
-            kv = r < 1461 - r ? r : 1461 - r;
-        }
-        const unsigned long long eq = bal(i < nf && kv == K);
-        const bool sel = i < nf && (kv < K || (kv == K && taken_eq + below(eq) < need));
-        taken_eq += popc(eq);
-        const unsigned long long sm = bal(sel);
-        if (sel) L->sel[nsel + below(sm)] = fa + i;
-        nsel += popc(sm);
-    }
-    wsync();
+    const int nf = fb - fa;  // <= 24: every fit observation is among its "24 closest"
     const int bnd = l >> 3, osub = l & 7;  // band-major: a band's 8 partial sums share a DPP row
-    // nsel <= 24: three fixed rounds of 8 observations, unrolled so the row / basis gathers of
-    // all three are in flight together
+    // three fixed rounds of 8 observations, unrolled so the row / basis gathers of all three are
+    // in flight together
     double e[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
         const int s2 = osub + 8 * r;
-        e[r] = (bnd < NB && s2 < nsel) ? resid_at(P, bnd, L->sel[s2]) : 0.0;
+        e[r] = (bnd < NB && s2 < nf) ? resid_at(P, bnd, fa + s2) : 0.0;
     }
     double ss = e[0] * e[0];
     ss += e[1] * e[1];
@@ -2847,7 +2830,7 @@ __device__ __forceinline__ void ring_rows(const Px &P, int x0) {
 }
 
 // Entries of the fit window whose closest-DOY bin lies within circular distance d of bin u
-// (L->hist2 = bin end positions after build_closest).
+// (L->hist2 = bin end positions after fit_bounds / build_buckets).
 __device__ __forceinline__ int cnt_within(const Lds *L, int nf, int u, int d) {
     // bins [u - d, u + d] (circular; 2 d + 1 < 1461 so at most one end wraps)
     int lo = u - d;
@@ -2866,6 +2849,9 @@ __device__ __forceinline__ int cnt_within(const Lds *L, int nf, int u, int d) {
 // ends), so within the blocks that bins [u - K, u + K] touch.  Their float block sums are each at
 // most (n 2^-24) below the exact sum of the rounded-up terms, which bound the squares from above;
 // inflated by 2^-9 they bound the exact -- and any computed -- sum of any 24 of them.
+// (the slack below -- 2^-10 of the total for the float prefixes, 2^-9 for the float block sums of
+// rounded-up terms -- covers at most 4096 terms per sum: CCDGPU_MAX_OBS)
+static_assert(CCDGPU_MAX_OBS <= 4096, "comp_bound / fit_bounds float slack sized for <= 4096 fit observations");
 __device__ __forceinline__ void comp_bound(int nf, int dref, const int (&bs)[NB], int nd, double (&cb)[NB]) {
     const Lds *L = &LDS();
     const int u = u1461(dref);
@@ -2908,160 +2894,6 @@ __device__ __forceinline__ void comp_bound(int nf, int dref, const int (&bs)[NB]
     }
 }
 
-// cs[bd] += p[s * FW + bd] for s = 0 .. cnt - 1, in order (cnt per lane).
-#ifndef CCD_RS
-#define CCD_RS 4
-#endif
-template <int FW>
-__device__ __forceinline__ void run_add(const GLOBAL_AS double *p, int cnt, double (&cs)[NB]) {
-    constexpr int RS = CCD_RS;
-    int s = 0;
-    for (; s + RS <= cnt; s += RS) {
-        double f[RS][FW];
-#pragma unroll
-        for (int u = 0; u < RS; ++u) {
-#pragma unroll
-            for (int bd = 0; bd < FW; ++bd) f[u][bd] = p[u * FW + bd];
-        }
-#pragma unroll
-        for (int u = 0; u < RS; ++u) {
-#pragma unroll
-            for (int bd = 0; bd < FW; ++bd) cs[bd] += f[u][bd];
-        }
-        p += RS * FW;
-    }
-    for (; s < cnt; ++s) {
-        double f[FW];
-#pragma unroll
-        for (int bd = 0; bd < FW; ++bd) f[bd] = p[bd];
-#pragma unroll
-        for (int bd = 0; bd < FW; ++bd) cs[bd] += f[bd];
-        p += FW;
-    }
-}
-
-// Per-lane find_closest_doy(period, ref, fit_window, 24) comparison rmse (change.lookforward):
-// the 24 fit-window observations closest in day of year to date dref, sqrt(sum r^2) / 4 per band,
-// from the bucket list and bucket-ordered squared residuals build_closest left (nf > 24).
-// Entries at distance < K form one circular run of bucket positions; at distance exactly K the
-// lowest fit-relative indices win (stable argsort).
-template <int FW>
-__device__ __forceinline__ void comp_lane(Px &P, int nf, int dref, double (&cs)[NB]) {
-    const Lds *L = &LDS();
-    PH_BEGIN(c1)
-    const int u = u1461(dref);
-    int lo = 0, hi = 730;  // smallest K with cnt_within(K) >= 24
-#pragma unroll
-    for (int it = 0; it < 10; ++it) {  // branch-free: a finished lane re-reads its own bin
-        const int mid = (lo + hi) >> 1;
-        const bool ge = cnt_within(L, nf, u, mid) >= 24;
-        const bool act = lo < hi;
-        hi = act && ge ? mid : hi;
-        lo = act && !ge ? mid + 1 : lo;
-    }
-    const int K = lo;
-    const int less = K > 0 ? cnt_within(L, nf, u, K - 1) : 0;
-    const int need = 24 - less;
-#pragma unroll
-    for (int bd = 0; bd < NB; ++bd) cs[bd] = 0.0;
-    const int s0 = K > 0 ? bstart(L, (u - K + 1 + 1461) % 1461) : 0;
-    PH_END(P, c1, 21)
-    PH_BEGIN(c2)
-    // The run is at most two contiguous stretches of bucket positions (it wraps at nf at most
-    // once): [s0w, s0w + n1) and [0, less - n1), summed in that order (= bucket order).  A stretch
-    // is read in rounds of RS rows from one running address, every row's loads at an immediate
-    // offset and issued before the first add; no per-row index arithmetic.
-    const int s0w = gidx(P, s0 >= nf ? s0 - nf : s0, nf, __LINE__);  // bucket position of row 0
-    const int lr = less < nf ? less : nf;
-    const int n1 = lr < nf - s0w ? lr : nf - s0w;
-    run_add<FW>(PFS(P) + (size_t)s0w * FW, n1, cs);
-    run_add<FW>(PFS(P), lr - n1, cs);
-    PH_END(P, c2, 22)
-    PH_BEGIN(c3)
-    const int b1 = (u - K + 1461) % 1461, b2 = (u + K) % 1461;
-    const int c1 = bcount(L, b1), c2 = K > 0 ? bcount(L, b2) : 0;
-    const int st1 = bstart(L, b1), st2 = bstart(L, b2);
-    const int T = c1 + c2;
-    // every entry at distance K is taken when there are no more of them than needed (no ranks)
-    const bool all_k = T <= need;
-    constexpr int TU = 8;
-    // Tb: the wave's largest T among the lanes on this path (uniform), so the entry loops below
-    // stop where every lane's entries end (T is 1 or 2 nearly always)
-    int Tb = 0;
-#pragma unroll
-    for (int e = 0; e < TU; ++e)
-        if (bal(T > e && T <= TU)) Tb = e + 1;
-    if (T <= TU) {
-        // up to 8 entries: their fit indices loaded at once and ranked in registers, then their
-        // squared residuals added in entry order (weight 0 for the entries not taken); ranks are
-        // needed only where more entries sit at distance K than are taken
-        int iv[TU], pe[TU];
-#pragma unroll
-        for (int e = 0; e < TU; ++e) {
-            pe[e] = e < T ? (e < c1 ? st1 + e : st2 + (e - c1)) : 0;
-            pe[e] = gidx(P, pe[e], nf, __LINE__);
-        }
-        const bool rk = bal(!all_k) != 0ull;
-#pragma unroll
-        for (int e = 0; e < TU; ++e) {
-            iv[e] = 0x7FFFFFFF;
-            if (rk && e < Tb) iv[e] = (!all_k && e < T) ? (int)PBK(P)[pe[e]] : 0x7FFFFFFF;
-        }
-        double ws[TU];
-#pragma unroll
-        for (int e = 0; e < TU; ++e) {
-            int rank = 0;
-            if (rk && e < Tb) {
-#pragma unroll
-                for (int f = 0; f < TU; ++f)
-                    if (f < Tb) rank += iv[f] < iv[e] ? 1 : 0;
-            }
-            ws[e] = (e < T && (all_k || rank < need)) ? 1.0 : 0.0;
-        }
-#pragma unroll
-        // two entries a round, their loads together; rounds past the wave's last entry skipped
-        for (int e0 = 0; e0 < TU; e0 += 2) {
-            if (e0 < Tb) {
-                double f[2][FW];
-#pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    const GLOBAL_AS double *fp = PFS(P) + (size_t)pe[e0 + u] * FW;
-#pragma unroll
-                    for (int bd = 0; bd < FW; ++bd) f[u][bd] = fp[bd];
-                }
-#pragma unroll
-                for (int u = 0; u < 2; ++u) {
-#pragma unroll
-                    for (int bd = 0; bd < FW; ++bd) cs[bd] = fma(f[u][bd], ws[e0 + u], cs[bd]);
-                }
-            }
-        }
-    }
-    for (int e = 0; e < (T <= TU ? 0 : T); ++e) {
-        const int pe = e < c1 ? st1 + e : st2 + (e - c1);
-        if (all_k) {
-            const GLOBAL_AS double *f = PFS(P) + (size_t)gidx(P, pe, nf, __LINE__) * FW;
-#pragma unroll
-            for (int bd = 0; bd < FW; ++bd) cs[bd] += f[bd];
-            continue;
-        }
-        const int ie = (int)PBK(P)[gidx(P, pe, P.n, __LINE__)];
-        int rank = 0;
-        for (int f2 = 0; f2 < T; ++f2) {
-            const int pf = f2 < c1 ? st1 + f2 : st2 + (f2 - c1);
-            rank += ((int)PBK(P)[gidx(P, pf, P.n, __LINE__)] < ie) ? 1 : 0;
-        }
-        if (rank < need) {
-            const GLOBAL_AS double *f = PFS(P) + (size_t)gidx(P, pe, nf, __LINE__) * FW;
-#pragma unroll
-            for (int bd = 0; bd < FW; ++bd) cs[bd] += f[bd];
-        }
-    }
-#pragma unroll
-    for (int bd = 0; bd < FW; ++bd) cs[bd] = sqrt(cs[bd]) / 4.0;
-    PH_END(P, c3, 23)
-}
-
 // change.lookforward.  The first steps (no model yet, or fewer than 24 observations in the
 // window) refit every step and run one at a time.  After that the model changes only at a refit
 // (window span >= 1.33 x the fitted span), so the steps between refits are evaluated in batches,
@@ -3090,11 +2922,7 @@ struct SpecFit {
 // index of (i, j), i <= j, in a row-major upper triangle of SPEC_PC columns
 __host__ __device__ constexpr int ut(int i, int j) { return i * SPEC_PC - i * (i - 1) / 2 + (j - i); }
 
-#ifdef CCD_SPEC_CALL
-__device__ __attribute__((noinline)) void spec_fits(Px &P, int a, int nw0, int V, SpecFit &F) {
-#else
 __device__ __forceinline__ void spec_fits(Px &P, int a, int nw0, int V, SpecFit &F) {
-#endif
     const ccdgpu_params &p = ARGS().p;
     Lds *L = &LDS();
     const int l = lane();
@@ -3330,9 +3158,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
     int hfa = -1, hfb = -1;  // fit window the closest-DOY buckets describe
     int nc_fit = nc;         // coefficients of the current fit
     bool exiting = false;  // the loop ends at its top
-#ifndef CCD_BUCKET_R2
     bool bnd_ok = false;   // fit_bounds' bins and blocks (L->hist2, L->blk) describe the current models
-#endif
     // One fit_models site for the three refits of this loop (an early step, the long-peek span
     // refit, the batched span refit): a path that needs a fit records it in fmode and continues,
     // the fit runs at the top of the next iteration, and the early / long-peek steps then resume
@@ -3344,19 +3170,16 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
         if (exiting) break;
         int ev = 0;  // single-step evaluation of this iteration: 1 early step, 2 long peek
         if (fmode) {
-#ifndef CCD_BUCKET_R2
             // fmode 4: the current models' bounds only (a batch of more than 24 fit observations
             // whose fit was an early step's: the first of a lookforward whose initialize window
             // holds more than 24), then that batch again
             if (fmode != 4) {
-#endif
-            fit_models(P, fa, fb, nc_fit, fmode == 1 || fb - fa <= 24);  // rmse: from build_closest when it runs
+            fit_models(P, fa, fb, nc_fit, fmode == 1 || fb - fa <= 24);  // rmse: from fit_bounds when it runs
             if (fmode == 1) {
                 have = true;
                 if (l < NB) L->comp[l] = L->rmse[l];  // early step: comparison rmse = model rmse
                 wsync();
             }
-#ifndef CCD_BUCKET_R2
             }
             // a span refit of more than 24 observations: its rmse and the batched steps'
             // comparison-rmse bounds from one pass over the window's residuals (the one site)
@@ -3366,7 +3189,6 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
                 fit_bounds(P, fa, fb, nc_fit);
                 PH_END(P, fbd, 12)  // (with build_buckets: the "closest bucket build" slot)
             }
-#endif
             ev = fmode == 3 || fmode == 4 ? 0 : fmode;
             fmode = 0;
         }
@@ -3399,9 +3221,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
                     fit_span = CDRU(P, b - 1) - CDRU(P, a);
                     if (installed != sp) {
                         spec_install(P, F, sp, b - a, nc);
-#ifndef CCD_BUCKET_R2
                         bnd_ok = false;
-#endif
                         installed = sp;
                         PH_COUNT(P, 37, 1)
                     }
@@ -3458,16 +3278,31 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
         }
         if (ev) {
             if (ev == 2) {
-                if (fb - fa > 24 && (hfa != fa || hfb != fb)) {
-#ifdef CCD_BUCKET_R2
-                    build_closest(P, fa, fb, nc_fit);
-#else
-                    build_buckets(P, fa, fb);  // (closest_doy_scan reads the bin ends)
-#endif
-                    hfa = fa;
-                    hfb = fb;
+                if (fb - fa > 24) {
+                    // the exact comparison rmse of the step as a batched step's (coop_comp)
+                    if (hfa != fa || hfb != fb) {
+                        build_buckets(P, fa, fb);
+                        hfa = fa;
+                        hfb = fb;
+                    }
+                    const unsigned dm = det_mask();
+                    const int nd = __builtin_popcount(dm);
+                    int bs[NB];
+                    unsigned rest = dm;
+#pragma unroll
+                    for (int t = 0; t < NB; ++t) {
+                        bs[t] = rest ? __builtin_ctz(rest) : 0;
+                        rest &= rest - 1u;
+                    }
+                    double o[NB];
+                    coop_comp(P, fa, fb - fa, CDR(P, b + k - 1), bs, nd, o);
+#pragma unroll
+                    for (int t = 0; t < NB; ++t)
+                        if (t < nd && l == bs[t]) L->comp[l] = o[t];
+                    wsync();
+                } else {
+                    closest_doy_scan(P, fa, fb);
                 }
-                closest_doy_scan(P, fa, fb, b + k - 1);
             }
             double m0;
             PH_BEGIN(ep)
@@ -3489,22 +3324,11 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
         }
         // ---- batch of up to B steps at window starts x0 .. x0 + B - 1 (model fixed)
         const int nf = fb - fa;
-#ifndef CCD_BUCKET_R2
         if (nf > 24 && !bnd_ok) {
             fmode = 4;  // the bounds at the loop's top, then this batch
             continue;
         }
-#endif
-#ifdef CCD_BUCKET_R2
-        if (nf > 24 && (hfa != fa || hfb != fb)) {
-            PH_BEGIN(hb)
-            build_closest(P, fa, fb, nc_fit);
-            PH_END(P, hb, 12)
-            hfa = fa;
-            hfb = fb;
-        }
-#endif
-        if (nf <= 24) closest_doy_scan(P, fa, fb, b);  // every fit observation: one comp for all steps
+        if (nf <= 24) closest_doy_scan(P, fa, fb);  // every fit observation: one comp for all steps
         PH_BEGIN(cl)
         const int x0 = b, m0 = P.m;
         PH_BEGIN(rr)
@@ -3529,7 +3353,6 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
         }
         const unsigned long long V = bal(valid);
         bool allc = false, outj = false;
-#ifndef CCD_BUCKET_R2
         if (nf > 24) {
             const unsigned dm = det_mask();
             const int nd = __builtin_popcount(dm);
@@ -3616,7 +3439,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
                         hfb = fb;
                     }
                     double o[NB];
-                    coop_comp(P, nf, rdl(drf, x), bs, nd, o);
+                    coop_comp(P, fa, nf, rdl(drf, x), bs, nd, o);
                     ++nres;
                     if (l == x) {
                         double irm[NB];
@@ -3630,12 +3453,10 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
                         else peek_mags<NB>(bs, irm, k, allc, outj);
                     }
                 }
-                PH_COUNT(P, 21, nres)  // (slot of comp_lane's search timer, unused on this path)
+                PH_COUNT(P, 21, nres)  // exact comparison rmse evaluations
                 PH_END(P, cmp, 14)
             }
-        } else
-#endif
-        if (valid) {
+        } else if (valid) {
             // comparison rmse per detection band: cs[s] for the s-th detection band bs[s]
             const unsigned dm = det_mask();
             const int nd = __builtin_popcount(dm);
@@ -3649,16 +3470,9 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
             double cs[NB];
 #pragma unroll
             for (int t = 0; t < NB; ++t) cs[t] = 0.0;
-            PH_BEGIN(cmp)
-            if (nf > 24) {
-                const int dref = CDR(P, x0 + l + k - 1);
-                if (fs_width(dm) == 5) comp_lane<5>(P, nf, dref, cs);
-                else comp_lane<7>(P, nf, dref, cs);
-            } else {
+            // (nf <= 24: every fit observation, one comparison rmse for all steps: closest_doy_scan)
 #pragma unroll
-                for (int t = 0; t < NB; ++t) cs[t] = L->comp[bs[t]];
-            }
-            PH_END(P, cmp, 14)
+            for (int t = 0; t < NB; ++t) cs[t] = L->comp[bs[t]];
             PH_BEGIN(mg)
             // change_magnitude: (r / max(vario, comp))^2 summed over the detection bands (in band
             // order), with the division as a multiply by the band's reciprocal (one division per
@@ -4067,10 +3881,8 @@ __device__ __forceinline__ void detect_body() {
     const int slot = blockIdx.x;
     const size_t nmax = (size_t)A.n_obs_max;  // per-slot scratch stride
     Px P;
-#ifndef CCD_PERIOD_IN_LDS
     P.cd = A.s_date + (size_t)slot * nmax;
     P.cr = reinterpret_cast<CRow *>(A.s_row) + (size_t)slot * nmax;
-#endif
     P.bad = 0;
     if (l < 4) lds.stat[l] = 0ull;
 #ifdef CCD_PHASE_TIMERS
@@ -4110,12 +3922,10 @@ __device__ __forceinline__ void detect_body() {
             // ... nor from the slot's global scratch
             for (size_t i = l; i < CCD_SLOT_F64(nmax); i += W) PFS(P)[i] = __longlong_as_double(-1ll);
             for (size_t i = l; i < nmax; i += W) PBK(P)[i] = 0xFFFFu;
-#ifndef CCD_PERIOD_IN_LDS
             for (size_t i = l; i < nmax; i += W) {
                 P.cd[i] = -1;
                 reinterpret_cast<uint4 *>(P.cr)[i] = uint4{~0u, ~0u, ~0u, ~0u};
             }
-#endif
             gsync();
         }
 #endif
@@ -4174,12 +3984,66 @@ __global__ __launch_bounds__(64, 3) __attribute__((flatten)) void ccd_detect_w3(
 __global__ __launch_bounds__(64, 4) __attribute__((flatten)) void ccd_detect_w4(int arg_slot) { detect_body(); }
 
 // ------------------------------------------------------------------ per-chip preparation
-// One 256-thread block per chip: stable rank of each date (ties by input position), sorted
-// dates, order, and the coefficient_matrix rows (w = 2 pi / avg_days_yr; cos/sin of w t, 2 w t,
-// 3 w t exactly as models/lasso.coefficient_matrix forms them).
+// numpy's argsort (kind='quicksort', numpy < 1.17 aquicksort -- the pinned reference's; restated
+// in oracle/ccd_oracle.c ccdoracle_np_argsort) of n <= CCDGPU_MAX_OBS keys in LDS, by one thread:
+// ord holds 0 .. n-1 on entry and the argsort on return.  Only chips with repeated dates get here
+// (without ties every sort gives the same order), so the sequential sort costs nothing elsewhere.
+__device__ void np_aquicksort_lds(const int64_t *v, uint16_t *ord, int n) {
+    int pl = 0, pr = n - 1;
+    int stack[64];  // (pl, pr) pairs: the larger part is pushed, so <= 2 log2(n) entries
+    int sp = 0;
+    for (;;) {
+        while (pr - pl > 15) {
+            const int pm = pl + ((pr - pl) >> 1);
+            uint16_t t;
+            if (v[ord[pm]] < v[ord[pl]]) { t = ord[pm]; ord[pm] = ord[pl]; ord[pl] = t; }
+            if (v[ord[pr]] < v[ord[pm]]) { t = ord[pr]; ord[pr] = ord[pm]; ord[pm] = t; }
+            if (v[ord[pm]] < v[ord[pl]]) { t = ord[pm]; ord[pm] = ord[pl]; ord[pl] = t; }
+            const int64_t vp = v[ord[pm]];
+            int pi = pl, pj = pr - 1;
+            t = ord[pm]; ord[pm] = ord[pj]; ord[pj] = t;
+            for (;;) {
+                do ++pi; while (v[ord[pi]] < vp);
+                do --pj; while (vp < v[ord[pj]]);
+                if (pi >= pj) break;
+                t = ord[pi]; ord[pi] = ord[pj]; ord[pj] = t;
+            }
+            t = ord[pi]; ord[pi] = ord[pr - 1]; ord[pr - 1] = t;
+            if (pi - pl < pr - pi) {
+                stack[sp] = pi + 1; stack[sp + 1] = pr;
+                pr = pi - 1;
+            } else {
+                stack[sp] = pl; stack[sp + 1] = pi - 1;
+                pl = pi + 1;
+            }
+            sp = sp + 2 < 64 ? sp + 2 : 62;
+        }
+        for (int i = pl + 1; i <= pr; ++i) {  // insertion sort
+            const uint16_t vi = ord[i];
+            const int64_t vv = v[vi];
+            int j = i;
+            while (j > pl && vv < v[ord[j - 1]]) {
+                ord[j] = ord[j - 1];
+                --j;
+            }
+            ord[j] = vi;
+        }
+        if (sp == 0) break;
+        sp -= 2;
+        pl = stack[sp];
+        pr = stack[sp + 1];
+    }
+}
+
+// One 256-thread block per chip: the argsort of the dates (ccd/__init__.py detect: numpy's
+// quicksort tie order, or with argsort_stable ties by input position), sorted dates, order, and
+// the coefficient_matrix rows (w = 2 pi / avg_days_yr; cos/sin of w t, 2 w t, 3 w t exactly as
+// models/lasso.coefficient_matrix forms them).  The stable rank of every date is computed in
+// parallel; a chip whose dates repeat then takes numpy's order from np_aquicksort_lds.
 __global__ __launch_bounds__(256) void ccd_prep(const int64_t *dates, const int32_t *chip_nobs,
                                                 const int64_t *chip_obs_off, double avg_days_yr,
-                                                int32_t *order, int64_t *sdates, double *basis) {
+                                                int argsort_stable, int32_t *order, int64_t *sdates,
+                                                double *basis) {
     const int chip = blockIdx.x;
     const int n = chip_nobs[chip];
     const int64_t off = chip_obs_off[chip];
@@ -4188,30 +4052,48 @@ __global__ __launch_bounds__(256) void ccd_prep(const int64_t *dates, const int3
     int64_t *sd = sdates + off;
     double *bs = basis + (size_t)off * CCD_BASIS_STRIDE;
     __shared__ int64_t sdl[CCDGPU_MAX_OBS];
+    __shared__ uint16_t perm[CCDGPU_MAX_OBS];  // sorted position -> input position
+    __shared__ int dup;
+    if (threadIdx.x == 0) dup = 0;
     for (int i = threadIdx.x; i < n; i += blockDim.x) sdl[i] = d[i];
     __syncthreads();
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         const int64_t di = sdl[i];
-        int rank = 0;
+        int rank = 0, eq = 0;
         for (int j = 0; j < n; ++j) {
             const int64_t dj = sdl[j];
             rank += (dj < di || (dj == di && j < i)) ? 1 : 0;
+            eq += dj == di ? 1 : 0;
         }
-        ord[rank] = i;
-        sd[rank] = di;
-        const double w = 2.0 * M_PI / avg_days_yr;
+        perm[rank] = (uint16_t)i;
+        if (eq > 1) dup = 1;
+    }
+    __syncthreads();
+    if (dup && !argsort_stable) {
+        if (threadIdx.x == 0) {
+            for (int i = 0; i < n; ++i) perm[i] = (uint16_t)i;
+            np_aquicksort_lds(sdl, perm, n);
+        }
+        __syncthreads();
+    }
+    const double w = 2.0 * M_PI / avg_days_yr;
+    for (int r = threadIdx.x; r < n; r += blockDim.x) {
+        const int i = perm[r];
+        const int64_t di = sdl[i];
+        ord[r] = i;
+        sd[r] = di;
         const double w12 = w * (double)di;
         const double w34 = 2.0 * w12;
         const double w56 = 3.0 * w12;
-        double *r = bs + (size_t)rank * CCD_BASIS_STRIDE;
-        r[0] = (double)di;
-        r[1] = cos(w12);
-        r[2] = sin(w12);
-        r[3] = cos(w34);
-        r[4] = sin(w34);
-        r[5] = cos(w56);
-        r[6] = sin(w56);
-        r[7] = 0.0;
+        double *row = bs + (size_t)r * CCD_BASIS_STRIDE;
+        row[0] = (double)di;
+        row[1] = cos(w12);
+        row[2] = sin(w12);
+        row[3] = cos(w34);
+        row[4] = sin(w34);
+        row[5] = cos(w56);
+        row[6] = sin(w56);
+        row[7] = 0.0;
     }
 }
 
@@ -4240,9 +4122,10 @@ __global__ __launch_bounds__(256) void ccd_scatter(const ccdgpu_segment *pool, c
 }  // namespace
 
 extern "C" int ccdk_prep(const int64_t *dates, int32_t n_chips, const int32_t *chip_nobs, const int64_t *chip_obs_off,
-                         double avg_days_yr, int32_t *order, int64_t *sdates, double *basis, void *stream) {
+                         double avg_days_yr, int32_t argsort_stable, int32_t *order, int64_t *sdates, double *basis,
+                         void *stream) {
     hipLaunchKernelGGL(ccd_prep, dim3(n_chips), dim3(256), 0, (hipStream_t)stream, dates, chip_nobs,
-                       chip_obs_off, avg_days_yr, order, sdates, basis);
+                       chip_obs_off, avg_days_yr, (int)argsort_stable, order, sdates, basis);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -4252,21 +4135,9 @@ extern "C" int ccdk_set_args(const CcdDetectArgs *host_args, int arg_slot, void 
                                   hipMemcpyHostToDevice, (hipStream_t)stream) == hipSuccess ? 0 : -1;
 }
 
-extern "C" int ccdk_period_in_lds(void) {
-#ifdef CCD_PERIOD_IN_LDS
-    return 1;
-#else
-    return 0;
-#endif
-}
-
 extern "C" size_t ccdk_lds_bytes(int32_t n_obs) {
-#ifdef CCD_PERIOD_IN_LDS
-    return sizeof(Lds) + (size_t)((4 * n_obs + 15) & ~15) + sizeof(CRow) * (size_t)n_obs;
-#else
     (void)n_obs;
     return sizeof(Lds);
-#endif
 }
 
 static const void *detect_fn(int variant) {

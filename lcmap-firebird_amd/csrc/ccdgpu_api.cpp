@@ -356,6 +356,8 @@ void ccdgpu_params_default(ccdgpu_params *p) {
     p->lasso_tol = 1e-4;
     p->clear_pct_threshold = 0.25;
     p->snow_pct_threshold = 0.75;
+    p->argsort_stable = 0;  // numpy quicksort tie order (include/ccdgpu.h)
+    p->reserved0 = 0;
 }
 
 int ccdgpu_device_count(int *count) {
@@ -496,7 +498,7 @@ int ccdgpu_init_copy_cus(int device, int copy_cus, ccdgpu_ctx **out) {
         return fail(CCDGPU_EINVAL, "more than " + std::to_string(CCD_ARG_SLOTS) + " live contexts in this process");
     }
     c->slots_per_cu = 16;
-    c->variant = ccdk_period_in_lds() ? 1 : 4;
+    c->variant = 4;
     if (const char *v = std::getenv("CCDGPU_KERNEL")) {
         if (v[0] == 'w' && v[1] >= '1' && v[1] <= '4' && v[2] == 0) c->variant = v[1] - '0';
     }
@@ -540,6 +542,7 @@ static int check_params(const ccdgpu_params *p) {
     if (p->lasso_max_iter < 1) return fail(CCDGPU_EINVAL, "lasso_max_iter must be >= 1");
     if ((p->detection_bands & ~0x7Fu) || (p->tmask_bands & ~0x7Fu))
         return fail(CCDGPU_EINVAL, "band masks must only use bits 0..6");
+    if (p->argsort_stable != 0 && p->argsort_stable != 1) return fail(CCDGPU_EINVAL, "argsort_stable must be 0 or 1");
     return 0;
 }
 
@@ -575,7 +578,7 @@ static int stage_alloc(ccdgpu_ctx *c, const ccdgpu_params *params, const Shape &
     if (occ <= 0) return fail(CCDGPU_EHIP, "detection kernel cannot be resident with " + std::to_string(ccdk_lds_bytes(sh.n_obs_max)) + " B of LDS");
     c->n_slots = (int32_t)std::min<int64_t>(c->total_pix, (int64_t)c->n_cu * std::min(occ, c->slots_per_cu));
     const size_t ns = (size_t)c->n_slots, no = (size_t)sh.n_obs_max;
-    const size_t nper = ccdk_period_in_lds() ? 1 : ns * no;  // global period scratch only when not in LDS
+    const size_t nper = ns * no;  // the compacted periods (dates, 16-byte rows) per slot
     if ((rc = c->s_date.ensure(nper)) || (rc = c->s_row.ensure(nper * 8)) ||
         (rc = c->s_f64.ensure(ns * CCD_SLOT_F64(no))) || (rc = c->s_bk.ensure(ns * no)))
         return rc;
@@ -1114,8 +1117,8 @@ static int launch(ccdgpu_ctx *c, CcdDetectArgs &a) {
     std::memcpy(hargs, &a, sizeof(a));
     if (ccdk_set_args(hargs, c->arg_slot, ax)) return fail(CCDGPU_EHIP, "copying kernel arguments to constant memory failed");
     HIPCHK(hipEventRecord(c->ev[0], ax));
-    if (ccdk_prep(c->in_dates, nc, c->chip_nobs.p, c->chip_obs_off.p, p.avg_days_yr, c->order.p, c->sdates.p, c->basis.p,
-                  ax))
+    if (ccdk_prep(c->in_dates, nc, c->chip_nobs.p, c->chip_obs_off.p, p.avg_days_yr, p.argsort_stable, c->order.p,
+                  c->sdates.p, c->basis.p, ax))
         return fail(CCDGPU_EHIP, std::string("prep launch: ") + hipGetErrorString(hipGetLastError()));
     HIPCHK(hipEventRecord(c->ev[1], ax));
     if (ax != c->stream) HIPCHK(hipStreamWaitEvent(c->stream, c->ev[1], 0));

@@ -61,6 +61,7 @@ typedef struct {
     ccdgpu_segment *segs;
     int nseg, segcap;
     int64_t fits, sweeps;
+    int32_t qs_deep; /* argsort parts past numpy 1.17's introsort depth limit (ccdoracle_np_argsort) */
 } pix_t;
 
 /* ------------------------------------------------------------------ small helpers */
@@ -102,6 +103,120 @@ static double chi2_5_ppf(double p) {
         if (chi2_5_cdf(mid) < p) lo = mid; else hi = mid;
     }
     return 0.5 * (lo + hi);
+}
+
+/* ------------------------------------------------------------------ numpy argsort (quicksort) */
+/* np.argsort(v) with numpy's default kind='quicksort' as the pinned reference image runs it:
+ * lcmap-pyccd's detect (ccd/__init__.py: argsort of the dates) and change.find_closest_doy
+ * (argsort of the day-of-year distances) call it, and their tie order decides which of equal
+ * dates is kept (mask_duplicate_values keeps the first) and which of equally close observations
+ * enter the comparison rmse.  The Dockerfile:4 conda image (Python 3.6, scikit-learn 0.18) carries
+ * a numpy < 1.17, whose aquicksort_<type> (numpy/core/src/npysort/quicksort.c.src) is restated
+ * here: median-of-3 pivot swapped to pr - 1, Sedgewick's partition (both scans stop on keys equal
+ * to the pivot), the larger part pushed, the smaller continued, insertion sort of parts of at
+ * most 16 (SMALL_QUICKSORT 15).  numpy 1.17 added a heapsort fallback for a part popped more than
+ * 2 floor(log2 n) partitions deep (introsort); *deep counts the parts that would have taken it
+ * (none on any input of the suite or the tiles -- tests/test_oracle.py).  numpy >= 1.25 sorts
+ * with x86-simd-sort on AVX-512 machines, another tie order.
+ * v: keys; tosort: 0..n-1 on entry, the argsort on return.  num > 0: only the parts overlapping
+ * positions [0, num) are sorted -- positions [0, num) end exactly as in the full sort (parts are
+ * disjoint ranges, each permuted only within itself). */
+#define NP_SMALL_QUICKSORT 15
+#define NP_QS_STACK 128
+static int np_msb(int n) {
+    int d = 0;
+    while (n >>= 1) d++;
+    return d;
+}
+/* [0] closest-DOY selections over more than 24 fit observations, [1] of them with ties across
+   the 24th position, [2] of those where the stable rule would take another set, [3] argsort
+   parts past numpy 1.17's depth limit (summed at the end of each pixel) */
+static int64_t g_qs_stats[4];
+void ccdoracle_argsort_stats(int64_t *out, int32_t reset) {
+    for (int i = 0; i < 4; ++i) {
+        out[i] = __atomic_load_n(&g_qs_stats[i], __ATOMIC_RELAXED);
+        if (reset) __atomic_store_n(&g_qs_stats[i], 0, __ATOMIC_RELAXED);
+    }
+}
+
+/* numpy's pairwise summation of a contiguous float64 array (np.sum / add.reduce,
+   numpy/core/src/umath/loops.c.src pairwise_sum_DOUBLE): below 8 terms in order; up to 128
+   eight running sums then ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) and the remainder in
+   order; above, the halves (n / 2 rounded down to a multiple of 8) summed recursively. */
+double ccdoracle_np_pairwise_sum(const double *a, int32_t n) {
+    if (n < 8) {
+        double res = 0.;
+        for (int i = 0; i < n; ++i) res += a[i];
+        return res;
+    } else if (n <= 128) {
+        double r[8], res;
+        int i;
+        for (int j = 0; j < 8; ++j) r[j] = a[j];
+        for (i = 8; i < n - (n % 8); i += 8)
+            for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+        res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; ++i) res += a[i];
+        return res;
+    } else {
+        int n2 = n / 2;
+        n2 -= n2 % 8;
+        return ccdoracle_np_pairwise_sum(a, n2) + ccdoracle_np_pairwise_sum(a + n2, n - n2);
+    }
+}
+static double np_pairwise_sum(const double *a, int n) { return ccdoracle_np_pairwise_sum(a, n); }
+
+void ccdoracle_np_argsort(const double *v, int32_t *tosort, int32_t n, int32_t num, int32_t *deep) {
+    int32_t *pl = tosort, *pr = tosort + n - 1;
+    int32_t *stack[NP_QS_STACK], **sptr = stack;
+    int depth[NP_QS_STACK / 2], *psdepth = depth;
+    int cdepth = np_msb(n) * 2;
+    const int32_t *lim = num > 0 ? tosort + num : tosort + n;  /* parts starting here are skipped */
+    if (n <= 1) return;
+    for (;;) {
+        if (cdepth < 0 && deep) ++*deep;
+        while ((pr - pl) > NP_SMALL_QUICKSORT) {
+            int32_t *pm = pl + ((pr - pl) >> 1), *pi, *pj, *pk, t;
+            double vp;
+            if (v[*pm] < v[*pl]) { t = *pm; *pm = *pl; *pl = t; }
+            if (v[*pr] < v[*pm]) { t = *pr; *pr = *pm; *pm = t; }
+            if (v[*pm] < v[*pl]) { t = *pm; *pm = *pl; *pl = t; }
+            vp = v[*pm];
+            pi = pl;
+            pj = pr - 1;
+            t = *pm; *pm = *pj; *pj = t;
+            for (;;) {
+                do ++pi; while (v[*pi] < vp);
+                do --pj; while (vp < v[*pj]);
+                if (pi >= pj) break;
+                t = *pi; *pi = *pj; *pj = t;
+            }
+            pk = pr - 1;
+            t = *pi; *pi = *pk; *pk = t;
+            /* push largest partition on stack (a part starting at or past lim is dropped) */
+            if (pi - pl < pr - pi) {
+                if (pi + 1 < lim) { *sptr++ = pi + 1; *sptr++ = pr; *psdepth++ = cdepth - 1; }
+                pr = pi - 1;
+            } else {
+                if (pl < lim) { *sptr++ = pl; *sptr++ = pi - 1; *psdepth++ = cdepth - 1; }
+                pl = pi + 1;
+            }
+            --cdepth;
+            if (pl >= lim) break;
+        }
+        if (pl < lim) {
+            for (int32_t *pi = pl + 1; pi <= pr; ++pi) {  /* insertion sort */
+                const int32_t vi = *pi;
+                const double vv = v[vi];
+                int32_t *pj = pi, *pk = pi - 1;
+                while (pj > pl && vv < v[*pk]) *pj-- = *pk--;
+                *pj = vi;
+            }
+        }
+        if (sptr == stack) break;
+        pr = *(--sptr);
+        pl = *(--sptr);
+        cdepth = *(--psdepth);
+    }
 }
 
 /* ------------------------------------------------------------------ Lasso (models/lasso.py) */
@@ -508,6 +623,7 @@ static void lookforward(pix_t *P, int *wa, int *wb) {
     double fit_span = period(P, b - 1) - period(P, a);
     double r[NB][CCDGPU_MAX_PEEK], comp[NB], mag[CCDGPU_MAX_PEEK];
     double *keys = (double *)malloc(sizeof(double) * 2 * (size_t)P->n);
+    int32_t *cord = (int32_t *)malloc(sizeof(int32_t) * ((size_t)P->n + 1)), cidx[24];
     int peek_start = b;
     while (b + P->peek < P->m || !have) {
         nc = num_coefs(p, b - a);
@@ -526,23 +642,56 @@ static void lookforward(pix_t *P, int *wa, int *wb) {
                 fit_span = period(P, b - 1) - period(P, a);
                 fit_models(P, fa, fb, nc);
             }
-            /* find_closest_doy(period, peek.stop - 1, fit_window, 24) */
+            /* find_closest_doy(period, peek.stop - 1, fit_window, 24): argsort(d_yr)[:24] */
             const int64_t ref = period_i(P, b + k - 1);
             const int nf = fb - fa;
-            for (int i = 0; i < nf; ++i) {
-                double d = (double)(period_i(P, fa + i) - ref);
-                keys[2 * i] = fabs(rint(d / 365.25) * 365.25 - d);
-                keys[2 * i + 1] = i;
-            }
-            qsort(keys, (size_t)nf, 2 * sizeof(double), cmp_key);
             const int take = nf < 24 ? nf : 24;
-            for (int band = 0; band < NB; ++band) {
-                double s = 0;
-                for (int j = 0; j < take; ++j) {
-                    double e = P->models[band].resid[(int)keys[2 * j + 1]];
-                    s += e * e;
+            if (p->argsort_stable) {
+                for (int i = 0; i < nf; ++i) {
+                    double d = (double)(period_i(P, fa + i) - ref);
+                    keys[2 * i] = fabs(rint(d / 365.25) * 365.25 - d);
+                    keys[2 * i + 1] = i;
                 }
-                comp[band] = sqrt(s) / 4.0;
+                qsort(keys, (size_t)nf, 2 * sizeof(double), cmp_key);
+                for (int j = 0; j < take; ++j) cidx[j] = (int32_t)keys[2 * j + 1];
+            } else {
+                for (int i = 0; i < nf; ++i) {
+                    double d = (double)(period_i(P, fa + i) - ref);
+                    keys[i] = fabs(rint(d / 365.25) * 365.25 - d);
+                    cord[i] = i;
+                }
+                ccdoracle_np_argsort(keys, cord, nf, 24, &P->qs_deep);
+                for (int j = 0; j < take; ++j) cidx[j] = cord[j];
+                if (nf > 24) {  /* exposure statistics (ccdoracle_argsort_stats) */
+                    const double kk = keys[cord[23]];
+                    int lt = 0, le = 0;
+                    for (int i = 0; i < nf; ++i) { lt += keys[i] < kk; le += keys[i] <= kk; }
+                    __atomic_add_fetch(&g_qs_stats[0], 1, __ATOMIC_RELAXED);
+                    if (le > 24) {
+                        /* ties straddle the 24th position: does the stable rule (lowest fit
+                           indices of the tied entries) take another set? */
+                        int need = 24 - lt, diff = 0, seen = 0;
+                        for (int i = 0; i < nf && seen < need; ++i)
+                            if (keys[i] == kk) {
+                                int in = 0;
+                                for (int j = lt; j < 24; ++j) in |= cord[j] == i;
+                                diff |= !in;
+                                ++seen;
+                            }
+                        __atomic_add_fetch(&g_qs_stats[1], 1, __ATOMIC_RELAXED);
+                        if (diff) __atomic_add_fetch(&g_qs_stats[2], 1, __ATOMIC_RELAXED);
+                    }
+                }
+            }
+            /* euclidean_norm(residual[closest]) / 4: numpy's pairwise sum of the squares in
+               argsort order (math_utils.euclidean_norm = np.sum(v ** 2) ** .5) */
+            for (int band = 0; band < NB; ++band) {
+                double sq[24];
+                for (int j = 0; j < take; ++j) {
+                    double e = P->models[band].resid[cidx[j]];
+                    sq[j] = e * e;
+                }
+                comp[band] = sqrt(np_pairwise_sum(sq, take)) / 4.0;
             }
         }
         for (int j = 0; j < k; ++j)
@@ -563,6 +712,7 @@ static void lookforward(pix_t *P, int *wa, int *wb) {
     }
     emit(P, period_i(P, a), period_i(P, b - 1), period_i(P, peek_start), b - a, (double)change, nc, mags);
     free(keys);
+    free(cord);
     *wa = a;
     *wb = b;
 }
@@ -747,6 +897,7 @@ done:
     *segs = P.segs;
     *nseg = P.nseg;
     *fits += P.fits;
+    if (P.qs_deep) __atomic_add_fetch(&g_qs_stats[3], P.qs_deep, __ATOMIC_RELAXED);
     *sweeps += P.sweeps;
     free(P.obs); free(P.mask); free(P.idx); free(cls);
     return rc;
@@ -789,8 +940,18 @@ int ccdoracle_detect_batch(const ccdgpu_params *p, int32_t n_pix, int32_t n_obs,
     out->error_pixel = -1;
     out->mask_words = (n_obs + 31) / 32;
     di_t *srt = (di_t *)malloc(sizeof(di_t) * (size_t)(n_obs > 0 ? n_obs : 1));
-    for (int i = 0; i < n_obs; ++i) { srt[i].d = dates[i]; srt[i].i = i; }
-    qsort(srt, (size_t)n_obs, sizeof(di_t), cmp_di);
+    if (p->argsort_stable) {
+        for (int i = 0; i < n_obs; ++i) { srt[i].d = dates[i]; srt[i].i = i; }
+        qsort(srt, (size_t)n_obs, sizeof(di_t), cmp_di);
+    } else {  /* ccd.detect: indices = np.argsort(dates) (numpy quicksort) */
+        double *dk = (double *)calloc((size_t)(n_obs > 0 ? n_obs : 1), sizeof(double));
+        int32_t *ord = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n_obs > 0 ? n_obs : 1));
+        for (int i = 0; i < n_obs; ++i) { dk[i] = (double)dates[i]; ord[i] = i; }
+        ccdoracle_np_argsort(dk, ord, n_obs, 0, NULL);
+        for (int i = 0; i < n_obs; ++i) { srt[i].d = dates[ord[i]]; srt[i].i = ord[i]; }
+        free(dk);
+        free(ord);
+    }
     out->sorted_dates = (int64_t *)malloc(sizeof(int64_t) * (size_t)(n_obs + 1));
     out->sort_index = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n_obs + 1));
     double *basis = (double *)malloc(sizeof(double) * 6 * (size_t)(n_obs + 1));

@@ -26,10 +26,15 @@ pyccd itself: no fixture in the reference holds a pyccd change-model result (SUR
 Every spec choice that could not be verified against the pinned pyccd source is a named
 parameter (``DEFAULTS`` below) so the GPU path and both oracles can be re-pinned by flipping it.
 
-Deliberate, documented deviations from the numpy reference (both are numpy-build dependent in
-pyccd, so no single "reference" answer exists):
-* ``argsort`` of dates and of closest-day-of-year distances uses a *stable* sort (ties by index);
-  numpy's default quicksort/x86-simd-sort breaks ties differently across builds.
+``argsort`` (the date sort of ``ccd.detect`` and ``change.find_closest_doy``) follows the tie
+order of numpy's default ``kind='quicksort'`` as the pinned reference image ran it: the
+Dockerfile:4 conda image (Python 3.6, scikit-learn 0.18) carries a numpy < 1.17, whose
+``aquicksort`` is restated literally in ``np1_argsort`` below (numpy >= 1.17 adds an introsort
+depth limit that no input here reaches; numpy >= 1.25 on AVX-512 hosts sorts with x86-simd-sort,
+a different tie order -- so this container's ``np.argsort`` is NOT the reference's).
+``ARGSORT='stable'`` restores rounds 1-5's stable rule (ties by index).
+
+Deliberate, documented deviation from the numpy reference:
 * a Tmask window spanning exactly 365 days gives a rank-deficient 5-column design (the 1/N-year
   harmonic equals the annual one); pyccd's QR leverage is then rounding noise.  Here the
   duplicated columns are dropped (the projection, hence every prediction, is unchanged).
@@ -78,6 +83,7 @@ DEFAULTS = dict(
     ADAPTIVE_PEEK=True,      # "ncompare": peek/threshold adapt to observation density (A.6)
     RMSE_DOF=False,          # rmse denominator n (False) or n - num_coefficients (True)
     KELVIN_TO_CELSIUS=True,  # standard procedure converts thermal K*10 -> C*100 (int16 wrap)
+    ARGSORT='quicksort',     # tie order of np.argsort: numpy < 1.17 quicksort ('stable': by index)
 )
 
 BANDS = ('blue', 'green', 'red', 'nir', 'swir1', 'swir2', 'thermal')
@@ -101,6 +107,112 @@ def get_params(params=None):
     if params:
         p.update(params)
     return p
+
+
+# --------------------------------------------------------------------------- numpy argsort
+def np1_argsort(v, num=None):
+    """np.argsort(v) (kind='quicksort') of numpy < 1.17: npysort/quicksort.c.src aquicksort,
+    restated literally -- median-of-3 pivot parked at pr - 1, Sedgewick's partition (both scans
+    stop on keys equal to the pivot), the larger part pushed, insertion sort of parts of at most
+    16.  ``num``: only the parts overlapping positions [0, num) are sorted; those positions end
+    exactly as in the full sort.  Returns (order, deep): deep counts the parts numpy 1.17's
+    introsort would have heap-sorted (popped past 2 floor(log2 n) partitions)."""
+    v = [float(x) for x in v]
+    n = len(v)
+    t = list(range(n))
+    if n <= 1:
+        return np.array(t, dtype=np.int64), 0
+    lim = n if num is None else min(num, n)
+    pl, pr = 0, n - 1
+    stack = []
+    cdepth = 2 * (n.bit_length() - 1)
+    deep = 0
+    while True:
+        if cdepth < 0:
+            deep += 1
+        while pr - pl > 15:
+            pm = pl + ((pr - pl) >> 1)
+            if v[t[pm]] < v[t[pl]]:
+                t[pm], t[pl] = t[pl], t[pm]
+            if v[t[pr]] < v[t[pm]]:
+                t[pr], t[pm] = t[pm], t[pr]
+            if v[t[pm]] < v[t[pl]]:
+                t[pm], t[pl] = t[pl], t[pm]
+            vp = v[t[pm]]
+            pi, pj = pl, pr - 1
+            t[pm], t[pj] = t[pj], t[pm]
+            while True:
+                pi += 1
+                while v[t[pi]] < vp:
+                    pi += 1
+                pj -= 1
+                while vp < v[t[pj]]:
+                    pj -= 1
+                if pi >= pj:
+                    break
+                t[pi], t[pj] = t[pj], t[pi]
+            t[pi], t[pr - 1] = t[pr - 1], t[pi]
+            cdepth -= 1
+            if pi - pl < pr - pi:
+                if pi + 1 < lim:
+                    stack.append((pi + 1, pr, cdepth))
+                pr = pi - 1
+            else:
+                if pl < lim:
+                    stack.append((pl, pi - 1, cdepth))
+                pl = pi + 1
+            if pl >= lim:
+                break
+        if pl < lim:
+            for i in range(pl + 1, pr + 1):
+                vi = t[i]
+                vv = v[vi]
+                j = i
+                while j > pl and vv < v[t[j - 1]]:
+                    t[j] = t[j - 1]
+                    j -= 1
+                t[j] = vi
+        if not stack:
+            break
+        pl, pr, cdepth = stack.pop()
+    return np.array(t, dtype=np.int64), deep
+
+
+_NP1_LIB = None
+
+
+def _np1_lib():
+    """oracle/libccdoracle.so's ccdoracle_np_argsort (the same restatement in C, checked equal to
+    np1_argsort by tests/test_oracle.py), or None when the library is not built."""
+    global _NP1_LIB
+    if _NP1_LIB is None:
+        import ctypes
+        import os
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libccdoracle.so')
+        lib = False
+        if os.path.exists(path):
+            lib = ctypes.CDLL(path)
+            lib.ccdoracle_np_argsort.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,
+                                                 ctypes.c_int32, ctypes.c_void_p]
+        _NP1_LIB = lib
+    return _NP1_LIB or None
+
+
+def argsort(v, p, num=None):
+    """np.argsort(v) with the reference's tie order (p.ARGSORT; see the module header)."""
+    v = np.ascontiguousarray(v, dtype=np.float64)
+    if p.ARGSORT == 'stable':
+        o = np.argsort(v, kind='stable')
+        return o if num is None else o[:num]
+    lib = _np1_lib()
+    if lib is not None:
+        o = np.arange(v.shape[0], dtype=np.int32)
+        lib.ccdoracle_np_argsort(v.ctypes.data, o.ctypes.data, int(v.shape[0]),
+                                 0 if num is None else int(num), None)
+        o = o.astype(np.int64)
+    else:
+        o = np1_argsort(v, num)[0]
+    return o if num is None else o[:num]
 
 
 # --------------------------------------------------------------------------- qa.py [ext]
@@ -229,6 +341,7 @@ def kelvin_to_celsius(thermals, scale=10):
 
 
 def euclidean_norm(v):
+    # np.sum: numpy's pairwise summation, in the order of v (for the comparison rmse: argsort order)
     v = np.asarray(v, dtype=np.float64)
     return math.sqrt(float(np.sum(v * v)))
 
@@ -453,10 +566,10 @@ def update_processing_mask(mask, index, window=None):
     return new_mask
 
 
-def find_closest_doy(dates, date_idx, window, num):
+def find_closest_doy(dates, date_idx, window, num, p):
     d_rt = dates[window] - dates[date_idx]
     d_yr = np.abs(np.round(d_rt / 365.25) * 365.25 - d_rt)
-    return np.argsort(d_yr, kind='stable')[:num]
+    return argsort(d_yr, p, num)[:num]
 
 
 def change_magnitude(residuals, variogram, comp_rmse):
@@ -572,7 +685,7 @@ def lookforward(dates, observations, model_window, processing_mask, variogram, p
                 models = [fitted_model(period[fit_window], s, p, num_coefs) for s in spectral_obs[:, fit_window]]
             residuals = np.array([spectral_obs[i, peek_window] - predict(models[i], period[peek_window], p)
                                   for i in range(observations.shape[0])])
-            closest = find_closest_doy(period, peek_window.stop - 1, fit_window, 24)
+            closest = find_closest_doy(period, peek_window.stop - 1, fit_window, 24, p)
             comp_rmse = np.array([euclidean_norm(models[i].residual[closest]) / 4 for i in db])
         magnitude = change_magnitude(residuals[db, :], variogram[db], comp_rmse)
         if detect_change(magnitude, p.CHANGE_THRESHOLD):
@@ -728,7 +841,7 @@ def detect(dates, blues, greens, reds, nirs, swir1s, swir2s, thermals, qas, para
     qas = np.asarray(qas)
     spectra = np.stack((blues, greens, reds, nirs, swir1s, swir2s, thermals))
     assert dates.ndim == 1 and dates.shape == qas.shape and dates.shape[0] == spectra.shape[1]
-    indices = np.argsort(dates, kind='stable')
+    indices = argsort(dates, p)
     dates = dates[indices]
     spectra = spectra[:, indices]
     qas = qas[indices]

@@ -7,7 +7,9 @@ hand-built edge cases; expected outputs are the restatement's change models and 
 
 The reference itself (lcmap-pyccd) is not importable in this container, so these
 vectors pin the GPU path and the C oracle to the restatement; the restatement is pinned by the
-reference's own boundary tests (tests/test_reference_boundary.py)."""
+reference's own boundary tests (tests/test_reference_boundary.py) and its argsort by a real
+numpy's quicksort (tests/golden/argsort/).  Default parameters = ARGSORT 'quicksort' (numpy's
+tie order, round 6); the *_stable cases keep the stable rule of rounds 1-5 covered."""
 import json
 import multiprocessing
 import os
@@ -145,6 +147,75 @@ def dense_case():
     return d, s, q
 
 
+def _tie_years_dates():
+    rng = np.random.default_rng(1461)
+    days = np.sort(rng.choice(1461, size=46, replace=False))
+    return np.concatenate([723900 + 1461 * c + days for c in range(9)]).astype(np.int64)
+
+
+def _tie_years_pixel(seed, d):
+    """one candidate pixel (ascending dates): seasonal cycle + random walk (+ steps every ~3 years
+    for odd seeds), optical bands kept inside (0, 10000) by redrawing"""
+    rng = np.random.default_rng(seed)
+    n = d.shape[0]
+    w = 2 * np.pi / 365.2425
+    base = np.array([500, 800, 700, 2800, 2000, 1200, 2950], dtype=np.float64)
+    amp = np.array([150, 200, 250, 600, 400, 300, 0], dtype=np.float64)
+    walk = np.array([25, 30, 35, 60, 50, 40, 0], dtype=np.float64)
+    while True:
+        y = (base[:, None] + amp[:, None] * np.cos(w * d[None, :] + rng.uniform(0, 2 * np.pi, (7, 1)))
+             + np.cumsum(rng.normal(0.0, 1.0, (7, n)), axis=1) * walk[:, None]
+             + rng.normal(0.0, 8.0, (7, n)))
+        if seed % 2:
+            for tb in range(int(d[0]) + 1000, int(d[-1]), 1100):
+                y[:, d >= tb] += rng.choice([-1, 1], size=(7, 1)) * rng.uniform(0.1, 0.3, (7, 1)) * base[:, None]
+        y[6] = base[6] + rng.normal(0.0, 20.0, n)  # thermal (K x 10) inside the valid range
+        if y[:6].min() >= 20 and y[:6].max() <= 9900:
+            break
+    r = rng.uniform(size=n)
+    qa = np.where(r < 0.85, 66, np.where(r < 0.97, 224, 1)).astype(np.uint16)
+    y[:, qa == 1] = -9999
+    return np.round(y).astype(np.int16), qa
+
+
+def _tie_years_outcome(args):
+    d, sp, qp, params = args
+    r = ccd_ref.detect(d, *[sp[b] for b in range(7)], qp, params=params)
+    return (tuple(r['processing_mask']),
+            tuple((m['start_day'], m['end_day'], m['break_day'], m['observation_count']) for m in r['change_models']))
+
+
+_TIE_YEARS = None
+
+
+def tie_years_case():
+    """Dates that repeat every 1461 days (4 years: the same 46 days of each 4-year cycle, for 36
+    years, descending): find_closest_doy's key |round(d/365.25)*365.25 - d| of two dates 1461
+    days apart is equal, so the fit-window entries come in groups of up to nine equal keys and
+    the 24 closest almost always cut a group -- numpy's argsort tie order (ARGSORT) decides which
+    of its entries enter the comparison rmse (change.lookforward).  The comparison rmse matters
+    only where it exceeds the variogram, so the spectra carry a random walk (small consecutive
+    differences, large residuals about any harmonic model).  Of 384 candidate pixels the first 8
+    whose restated outputs differ between the quicksort and the stable tie rule are kept, and 8
+    whose outputs agree."""
+    global _TIE_YEARS
+    if _TIE_YEARS is None:
+        d = _tie_years_dates()
+        NC = 384
+        cands = [_tie_years_pixel(1000 + k, d) for k in range(NC)]
+        jobs = [(d, sp, qp, par) for sp, qp in cands for par in (None, {'ARGSORT': 'stable'})]
+        with multiprocessing.Pool(min(8, os.cpu_count() or 1)) as pool:
+            outs = pool.map(_tie_years_outcome, jobs)
+        diff = [k for k in range(NC) if outs[2 * k] != outs[2 * k + 1]]
+        same = [k for k in range(NC) if outs[2 * k] == outs[2 * k + 1]]
+        pick = diff[:8] + same[:16 - len(diff[:8])]
+        print('tie_years: %d of %d candidates differ between the tie rules; kept %s' % (len(diff), NC, pick))
+        s = np.stack([cands[k][0] for k in pick], axis=1)
+        q = np.stack([cands[k][1] for k in pick], axis=0)
+        _TIE_YEARS = (d[::-1].copy(), s[:, :, ::-1].copy(), q[:, ::-1].copy())
+    return _TIE_YEARS
+
+
 def main():
     only = set(sys.argv[1:])
     cases = {
@@ -158,6 +229,9 @@ def main():
     for name, inp in edge_cases().items():
         cases[name] = (inp, None)
     cases['dense_daily'] = (dense_case(), None)
+    cases['tie_years'] = (tie_years_case(), None)
+    cases['tie_years_stable'] = (tie_years_case(), {'ARGSORT': 'stable'})
+    cases['dup_shuffled_stable'] = (cases['dup_shuffled'][0], {'ARGSORT': 'stable'})
     with multiprocessing.Pool(min(8, os.cpu_count() or 1)) as pool:
         for name, ((d, s, q), params) in cases.items():
             if only and name not in only:
@@ -165,8 +239,9 @@ def main():
             jobs = [(d, s[:, p], q[p], params) for p in range(q.shape[0])]
             results = pool.map(run_pixel, jobs)
             out = to_arrays(results, d.shape[0])
+            order = ccd_ref.argsort(d, ccd_ref.get_params(params)).astype(np.int32)  # ccd.detect's date sort
             np.savez_compressed(os.path.join(HERE, name + '.npz'), dates=d, spectra=s, qa=q,
-                                params=np.array(json.dumps(params or {})), **out)
+                                params=np.array(json.dumps(params or {})), sort_index=order, **out)
             print(name, 'pixels', q.shape[0], 'obs', d.shape[0], 'segments', len(out['segments']),
                   'procedures', np.bincount(out['procedure'], minlength=3).tolist(), flush=True)
 

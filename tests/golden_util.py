@@ -25,7 +25,8 @@ def load(name):
     u.mask = np.unpackbits(z['mask'], axis=1, bitorder='little')[:, :u.n_obs].astype(bool)
     u.procedure = z['procedure']
     u.probs = z['probs']
-    order = np.argsort(d, kind='stable')
+    # the restatement's date sort (numpy's quicksort tie order unless ARGSORT 'stable')
+    order = z['sort_index'].astype(np.int64) if 'sort_index' in z.files else np.argsort(d, kind='stable')
     u.sorted_dates = d[order]
     u.sort_index = order.astype(np.int32)
     u.error_pixel = -1

@@ -90,3 +90,58 @@ def test_oracle_peek_overflow_is_an_error():
     rc, _ = oracle_ctypes.detect_batch(d, s[:, :2], q[:2], params={'PEEK_SIZE': 8}, threads=2)
     assert rc == abi.E_OVERFLOW
     assert abi.MAX_PEEK == 96
+
+
+# ---- the reference's argsort tie order (numpy < 1.17 quicksort)
+def _np126_vectors():
+    import os
+    z = np.load(os.path.join(golden_util.GOLDEN_DIR, 'argsort', 'np126_vectors.npz'))
+    off = np.concatenate([[0], np.cumsum(z['lens'])])
+    return [(z['keys'][a:b], z['argsort'][a:b]) for a, b in zip(off[:-1], off[1:])]
+
+
+def test_argsort_restatements_match_real_numpy_quicksort():
+    """ccdoracle_np_argsort (C) and ccd_ref.np1_argsort (literal Python port) reproduce the tie
+    order of a real numpy's C quicksort (numpy 1.26.4, AVX-512 dispatch off: the aquicksort of
+    numpy < 1.25 -- vectors made by tests/golden/argsort/check_np126.py) on closest-DOY keys and
+    dates with duplicates, whole and as the first 24 positions of the partial sort."""
+    lib = ccd_ref._np1_lib()
+    assert lib, 'oracle/libccdoracle.so not built'
+    cases = _np126_vectors()
+    assert len(cases) >= 100
+    for v, ref in cases:
+        n = v.shape[0]
+        o, deep = ccd_ref.np1_argsort(v)
+        assert deep == 0
+        assert np.array_equal(o, ref)
+        c = np.arange(n, dtype=np.int32)
+        lib.ccdoracle_np_argsort(np.ascontiguousarray(v).ctypes.data, c.ctypes.data, n, 0, None)
+        assert np.array_equal(c, ref)
+        if n > 24:
+            c = np.arange(n, dtype=np.int32)
+            lib.ccdoracle_np_argsort(np.ascontiguousarray(v).ctypes.data, c.ctypes.data, n, 24, None)
+            assert np.array_equal(c[:24], ref[:24])
+            assert np.array_equal(ccd_ref.np1_argsort(v, 24)[0][:24], ref[:24])
+
+
+def test_argsort_stable_option_and_differs_on_ties():
+    p = ccd_ref.get_params({'ARGSORT': 'stable'})
+    q = ccd_ref.get_params()
+    assert q.ARGSORT == 'quicksort'
+    v = np.array([3., 1., 2., 1., 3., 1.] * 5)
+    assert np.array_equal(ccd_ref.argsort(v, p), np.argsort(v, kind='stable'))
+    o = ccd_ref.argsort(v, q)
+    assert np.array_equal(v[o], np.sort(v))
+    assert not np.array_equal(o, np.argsort(v, kind='stable'))  # quicksort breaks these ties otherwise
+
+
+def test_pairwise_sum_is_numpys():
+    """the C oracle's comparison-rmse sum is numpy's pairwise add.reduce, bit for bit"""
+    import ctypes
+    lib = ccd_ref._np1_lib()
+    lib.ccdoracle_np_pairwise_sum.restype = ctypes.c_double
+    lib.ccdoracle_np_pairwise_sum.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+    rng = np.random.default_rng(3)
+    for n in list(range(0, 40)) + [127, 128, 129, 300, 1000]:
+        a = rng.standard_normal(n) ** 2 * 10.0 ** rng.integers(-3, 6, n)
+        assert lib.ccdoracle_np_pairwise_sum(np.ascontiguousarray(a).ctypes.data, n) == float(np.sum(a))

@@ -36,7 +36,8 @@ for a, b in (('SQ_WAIT_ANY', 'SQ_WAVE_CYCLES'), ('SQ_ACTIVE_INST_ANY', 'SQ_WAVE_
         out[a + '/' + b] = out[a] / out[b]
 print(json.dumps(out, indent=1))
 
-# --write <workload>: record the per-launch HBM traffic for bench.py's roofline.traffic field
+# --write <workload> [--out pmc_<name>.json]: record the per-launch HBM traffic and counters for
+# bench.py's roofline (bench.py reads every profiles/pmc_*.json and matches 'workload')
 if '--write' in sys.argv:
     wl = sys.argv[sys.argv.index('--write') + 1]
     rec = {'workload': wl, 'kernel': kern, 'source': 'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, tag %s' % tag,
@@ -45,6 +46,7 @@ if '--write' in sys.argv:
            'correction': 'FETCH_SIZE x 2 (gfx950 reports half the bytes of wide reads, MI355X_MICROARCH.md HBM section); WRITE_SIZE as read',
            'counters': {k: v for k, v in out.items() if k.isupper() or k.startswith('SQ_') or k.startswith('TC')}}
     os.makedirs(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'profiles'), exist_ok=True)
-    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'profiles', 'pmc_detect.json')
+    name = sys.argv[sys.argv.index('--out') + 1] if '--out' in sys.argv else 'pmc_detect.json'
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'profiles', name)
     json.dump(rec, open(path, 'w'), indent=1)
     print('wrote', path)
