@@ -64,6 +64,7 @@ def parse():
     ap.add_argument('--contexts', type=int, default=2,
                     help='contexts per GPU running steps concurrently (each stages the same chips)')
     ap.add_argument('--cpu-seconds', type=float, default=12.0, help='target CPU-baseline sample time')
+    ap.add_argument('--cpu-min-pixels', type=int, default=20000, help='smallest CPU-baseline sample (pixels)')
     ap.add_argument('--restatement-pixels', type=int, default=1600,
                     help='pixels of the pyccd-structured restatement baseline sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -97,6 +98,10 @@ def parse():
                          '(tile.parity_sample; 0 = none)')
     ap.add_argument('--roofline-launches', type=int, default=3,
                     help='single-context launches of the resident batch timed for the roofline (per-launch duration)')
+    ap.add_argument('--no-config-legs', action='store_true',
+                    help='skip the short resident legs of the other synthetic configs (resident_c2 / _c4 / _c5)')
+    ap.add_argument('--config-leg-chips', type=int, default=16, help='chips per GPU of each other-config resident leg')
+    ap.add_argument('--config-leg-steps', type=int, default=3, help='timed steps of each other-config resident leg')
     ap.add_argument('--share-device', action='store_true',
                     help='rehearsal only: ranks beyond the device count share devices (LOCAL_RANK mod count)')
     return ap.parse_args()
@@ -228,6 +233,20 @@ def main():
         a2 = copy.copy(args)
         a2.tile_encode = 'lossless'
         tl_lossless = tile_leg(a2, cfg, rank, world, device, dist)
+    others = {}
+    if not args.no_config_legs:
+        # BASELINE.json's other single-GPU configs (C2 sparse cadence, C4 masked / snow, C5
+        # change-dense): a short resident leg each, with its own roofline and workload key
+        import copy
+        for k in sorted(CONFIG_NAMES):
+            if k == args.config:
+                continue
+            a4 = copy.copy(args)
+            a4.config, a4.chips, a4.steps, a4.warmup = k, args.config_leg_chips, args.config_leg_steps, 1
+            a4.roofline_launches = 2
+            r = resident_leg(a4, synth.config(k), rank, world, device, dist)
+            r.pop('batch')
+            others['resident_c%d' % k] = r
     if rank == 0:
         out = {
             'metric': 'pixels/sec change-detected (CONUS ARD tile) at 1/2/4/8 MI355X; FP64 VALU %',
@@ -272,6 +291,7 @@ def main():
             'resident': res,
             'tile': tl,
         }
+        out.update(others)
         if north is not None:
             out['north_star_tile'] = {k: north.get(k) for k in (
                 'value', 'unit', 'seconds', 'chips', 'pixels', 'chips_per_rank_done', 'tail_seconds_per_rank',
@@ -370,24 +390,19 @@ def resident_leg(args, cfg, rank, world, device, dist, batch=None):
     achieved_tf = flops / (launch_ms * 1e-3) / 1e12
     mix = cadence_mix(batch)
     workload_key = 'config%d_chips%d_mix%s' % (args.config, len(ids), '-'.join('%dx%d' % (k, v) for k, v in sorted(mix.items())))
-    traffic, pmc_c = None, {}
-    pmc_path = os.path.join(ROOT, 'profiles', 'pmc_detect.json')
-    if os.path.exists(pmc_path):
-        try:
-            pmc = json.load(open(pmc_path))
-            if pmc.get('workload') == workload_key:
-                traffic = pmc.get('hbm_bytes_per_launch')
-                pmc_c = pmc.get('counters', {})
-        except Exception:
-            traffic, pmc_c = None, {}
+    pmc_file, pmc = pmc_record(workload_key)
+    traffic = pmc.get('hbm_bytes_per_launch')
+    pmc_c = pmc.get('counters', {})
     # occupancy of the persistent launch: its resident wave slots over the SIMDs (4 per CU), and
     # the same from the PMC pass (SQ_WAVES per launch); FP64 share of the VALU instructions
-    waves_per_simd = last.get('wave_slots', 0) / (4.0 * last['n_cu']) if last.get('n_cu') else None
+    n_cu = last.get('n_cu')
+    waves_per_simd = last.get('wave_slots', 0) / (4.0 * n_cu) if n_cu else None
     f64 = sum(pmc_c.get(k, 0.0) for k in ('SQ_INSTS_VALU_ADD_F64', 'SQ_INSTS_VALU_FMA_F64', 'SQ_INSTS_VALU_MUL_F64',
                                           'SQ_INSTS_VALU_TRANS_F64'))
     fp64_share = f64 / pmc_c['SQ_INSTS_VALU'] if pmc_c.get('SQ_INSTS_VALU') else None
-    pmc_waves = pmc_c['SQ_WAVES'] / (4.0 * last['n_cu']) if pmc_c.get('SQ_WAVES') and last.get('n_cu') else None
+    pmc_waves = pmc_c['SQ_WAVES'] / (4.0 * n_cu) if pmc_c.get('SQ_WAVES') and n_cu else None
     wait_share = pmc_c.get('SQ_WAIT_ANY/SQ_WAVE_CYCLES')
+    hw = hardware_fp64(pmc_c, launch_ms, n_cu)
     return {
         'value': value, 'unit': 'pixels/s', 'steps': args.steps, 'ms_per_step': elapsed / args.steps * 1e3,
         'workload': '%s; %d tile chips per GPU spread evenly over the tile (chip %d, %d, ..., %d; %s), one ragged batch '
@@ -427,11 +442,64 @@ def resident_leg(args, cfg, rank, world, device, dist, batch=None):
                           '_pmc = SQ_WAVES per launch of the PMC pass',
             'fp64_share_of_valu': fp64_share,
             'wait_share_of_wave_cycles': wait_share,
+            'pmc_record': pmc_file,
+            'hw_fp64_lane_flops': hw.get('lane_flops'),
+            'hw_fp64_frac': hw.get('frac'),
+            'valu_busy': hw.get('valu_busy'),
+            'valu_issue_model': hw.get('valu_issue_model'),
+            'hw_note': hw.get('note'),
         },
         'segments_per_step': segs * world,
         'prep_ms_per_launch': float(np.mean(prep_ms)),
         'batch': batch,
     }
+
+
+def pmc_record(workload_key):
+    """(file name, record) of the committed PMC pass (profiles/pmc_*.json, written by
+    tools/pmc_summary.py --write) taken on the same workload key, or (None, {})."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'pmc_*.json')))
+    # pmc_detect.json (the C3 headline key) first, then the per-config records
+    paths.sort(key=lambda p: os.path.basename(p) != 'pmc_detect.json')
+    for p in paths:
+        try:
+            rec = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        if isinstance(rec, dict) and rec.get('workload') == workload_key:
+            return os.path.relpath(p, ROOT), rec
+    return None, {}
+
+
+def hardware_fp64(c, launch_ms, n_cu):
+    """What the FP64 pipe really issued, from the PMC pass of the same workload key (beside the
+    op-count frac, which credits modelled flops -- e.g. the closest-DOY work the comparison-rmse
+    bounds skip, DESIGN.md §4 "Roofline"):
+      lane_flops = 64 x (ADD + MUL + 2 FMA + TRANS)_F64 wave instructions (every lane counted, as if
+                   EXEC were full: an upper bound of the lane flops the pipe did);
+      frac       = lane_flops / the un-profiled launch duration / the FP64 vector peak;
+      valu_busy  = SQ_ACTIVE_INST_VALU (quad-cycles, summed over waves) x 4 / (SIMDs x the launch's
+                   cycles, GRBM_GUI_ACTIVE / 8 XCDs): share of SIMD cycles with a VALU issue;
+      valu_issue_model = (4 cycles per FP64 + 2 per other VALU wave instruction) / SIMD cycles."""
+    if not c or not launch_ms:
+        return {}
+    f64 = {k: c.get('SQ_INSTS_VALU_%s_F64' % k, 0.0) for k in ('ADD', 'MUL', 'FMA', 'TRANS')}
+    lane = 64.0 * (f64['ADD'] + f64['MUL'] + 2.0 * f64['FMA'] + f64['TRANS'])
+    out = {'lane_flops': lane, 'frac': lane / (launch_ms * 1e-3) / (FP64_PEAK_TFLOPS * 1e12),
+           'note': 'hw_fp64_lane_flops = 64 x (ADD + MUL + 2 FMA + TRANS) F64 wave instructions of the PMC pass '
+                   '(full-EXEC upper bound); hw_fp64_frac = that / kernel_ms_per_launch / peak; valu_busy = '
+                   'SQ_ACTIVE_INST_VALU x 4 / (4 SIMDs x CUs x GRBM_GUI_ACTIVE / 8); valu_issue_model = '
+                   '(4 x F64 + 2 x other VALU instructions) / the same SIMD cycles'}
+    simds = 4.0 * n_cu if n_cu else None
+    cyc = c.get('GRBM_GUI_ACTIVE', 0.0) / 8.0
+    if simds and cyc:
+        if c.get('SQ_ACTIVE_INST_VALU'):
+            out['valu_busy'] = c['SQ_ACTIVE_INST_VALU'] * 4.0 / (simds * cyc)
+        if c.get('SQ_INSTS_VALU'):
+            nf = sum(f64.values())
+            out['valu_issue_model'] = (4.0 * nf + 2.0 * (c['SQ_INSTS_VALU'] - nf)) / (simds * cyc)
+    return out
 
 
 def max_over_ranks(x, dist):
@@ -451,6 +519,66 @@ def _cgroup_cpu():
             return {k: int(v) for k, v in (ln.split() for ln in f if ln.strip())}
     except (OSError, ValueError):
         return None
+
+
+class _ThreadCpu(object):
+    """CPU seconds of this process's threads over a timed region, by thread (the host side of the
+    tile: who uses the box's CPU share).  A sampler thread reads /proc/self/task/*/stat every
+    ``period`` s and keeps each thread's last reading (threads that end inside the region -- the
+    runner's workers -- are counted up to their last sample); Python threads are named by
+    threading.enumerate(), native threads (OpenMP encoders, the HIP runtime) by their comm."""
+
+    def __init__(self, period=0.2):
+        import threading
+        self.period = period
+        self._stop = threading.Event()
+        self._first, self._last, self._names = {}, {}, {}
+        self._tick = float(os.sysconf('SC_CLK_TCK'))
+        self._th = threading.Thread(target=self._run, daemon=True, name='bench-cpu-sampler')
+
+    def _sample(self):
+        import threading
+        names = {t.native_id: t.name for t in threading.enumerate() if getattr(t, 'native_id', None)}
+        base = '/proc/self/task'
+        for tid in os.listdir(base):
+            try:
+                with open('%s/%s/stat' % (base, tid)) as f:
+                    txt = f.read()
+            except OSError:
+                continue
+            comm = txt[txt.index('(') + 1:txt.rindex(')')]
+            f = txt[txt.rindex(')') + 2:].split()
+            cpu = (int(f[11]) + int(f[12])) / self._tick  # utime + stime
+            t = int(tid)
+            self._first.setdefault(t, cpu if not self._last else 0.0)
+            self._last[t] = cpu
+            self._names[t] = names.get(t, self._names.get(t, comm))
+
+    def _run(self):
+        while not self._stop.wait(self.period):
+            self._sample()
+
+    def start(self):
+        self._sample()
+        self._th.start()
+        return self
+
+    def stop(self):
+        self._stop.set()
+        self._th.join()
+        self._sample()
+        by = {}
+        for t, cpu in self._last.items():
+            name = self._names[t]
+            # group numbered threads (ccd-worker-0, Thread-3 ...) and same-comm native threads
+            key = name.rstrip('0123456789').rstrip('-_ ') or name
+            by[key] = by.get(key, 0.0) + cpu - self._first.get(t, 0.0)
+        total = sum(by.values())
+        return {'total_s': round(total, 2),
+                'by_thread_s': {k: round(v, 2) for k, v in sorted(by.items(), key=lambda kv: -kv[1]) if v >= 0.05},
+                'threads_seen': len(self._last),
+                'note': 'utime + stime per thread of this process over the timed tile (sampled every %.1f s; '
+                        'native threads by comm: OpenMP encode threads and HIP runtime threads)' % self.period}
 
 
 class _Offset(object):
@@ -571,12 +699,14 @@ def tile_leg(args, cfg, rank, world, device, dist, split=False):
     gen0 = src.generate_seconds
     enc0 = (esrc.bytes_raw, esrc.bytes_sent, esrc.encode_seconds) if encode else (0, 0, 0.0)
     cg0 = _cgroup_cpu()
+    tcpu = _ThreadCpu().start()
     t = time.perf_counter()
     res = run(total, src_timed, sample=True)
     ctxs[0].synchronize()
     if dist is not None:
         dist.barrier()
     el = max_over_ranks(time.perf_counter() - t, dist)
+    thread_cpu = tcpu.stop()
     parity = None
     if sample_sink[0] is not None:
         parity = tile_parity_sample(sample_sink[0], src, cfg, mode, dist)
@@ -597,6 +727,8 @@ def tile_leg(args, cfg, rank, world, device, dist, split=False):
     for c in ctxs:
         c.close()
     src.close()
+    if encode:
+        esrc.close()  # the pinned encode buffers go now, not at interpreter exit
     if res is None:
         return None
     px = sum(c['n_pix'] for c in res['chips'])
@@ -617,6 +749,7 @@ def tile_leg(args, cfg, rank, world, device, dist, split=False):
             'gpu_numa_node': numa_node, 'host_threads_bound_to_gpu_node': not args.tile_no_numa,
             'transport_encoding': enc_stats,
             'cgroup_cpu_during_tile_s': cg,
+            'thread_cpu_during_tile_rank0': thread_cpu,
             'source_prepare_seconds': round(prep_s, 2),
             'generate_seconds_rank0': round(gen_s, 3),
             'pinned_pool_batches': src.allocated,
@@ -728,41 +861,59 @@ def host_cpus():
 
 def cpu_baseline(batch, args):
     """C restatement oracle (oracle/libccdoracle.so) on a bounded pixel sample of the workload's
-    chips that share chip 0's date vector, OpenMP over pixels, on the box's CPU share of one GPU
-    (OMP_NUM_THREADS; the cgroup quota -- every affinity CPU would only time-slice on it)."""
+    chips in the tile's own cadence mix -- every date vector of the batch (base cadence and
+    sidelap) gets its share of the sample in proportion to its chips -- at least
+    ``--cpu-min-pixels`` pixels, OpenMP over pixels, on the box's CPU share of one GPU
+    (OMP_NUM_THREADS; the cgroup quota -- every affinity CPU would only time-slice on it).
+    value = all sampled pixels / the summed oracle time of the groups."""
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
     import oracle_ctypes
     thr, info = host_cpus()
-    dates = batch.chip(0)[0]
-    same = [c for c in range(batch.n_chips) if np.array_equal(batch.chip(c)[0], dates)]
+    groups = {}
+    for c in range(batch.n_chips):
+        groups.setdefault(int(batch.n_obs[c]), []).append(c)
 
-    def sample(n):
-        """the first n pixels of the chips in `same`, as one (spectra, qa) pair"""
+    def sample(chips, n):
+        """the first n pixels of `chips` (sharing one date vector), as one (spectra, qa) pair; the
+        pixels of every chip are spread over it (a stride), not its first rows only"""
         S, Q, got = [], [], 0
-        for c in same:
+        per = -(-n // len(chips))
+        for c in chips:
             _, s, q = batch.chip(c)
-            k = min(n - got, s.shape[1])
-            S.append(s[:, :k])
-            Q.append(q[:k])
+            k = min(n - got, per, s.shape[1])
+            sel = np.linspace(0, s.shape[1] - 1, k).astype(np.int64) if k > 0 else np.zeros(0, np.int64)
+            S.append(s[:, sel])
+            Q.append(q[sel])
             got += k
             if got >= n:
                 break
         return np.ascontiguousarray(np.concatenate(S, axis=1)), np.ascontiguousarray(np.concatenate(Q, axis=0))
 
-    n_probe = min(32 * thr, PIXELS_PER_CHIP * len(same))
-    S, Q = sample(n_probe)
-    t = time.perf_counter()
-    oracle_ctypes.detect_batch(dates, S, Q, threads=thr)
-    rate = n_probe / (time.perf_counter() - t)
-    secs = args.cpu_seconds
-    n = int(min(PIXELS_PER_CHIP * len(same), max(n_probe, rate * secs)))
-    S, Q = sample(n)
-    t = time.perf_counter()
-    oracle_ctypes.detect_batch(dates, S, Q, threads=thr)
-    el = time.perf_counter() - t
-    out = {'value': n / el, 'unit': 'pixels/s', 'cores': thr, 'kind': 'port',
-           'sample': 'first %d pixels of the workload chips sharing chip 0\'s %d dates (%.1f s), C restatement oracle, '
-                     'OpenMP %d threads' % (n, dates.shape[0], el, thr)}
+    # probe the rate on a small mixed sample, then size the sample to ~cpu_seconds (>= the minimum)
+    probe_t, probe_n = 0.0, 0
+    for nobs, chips in groups.items():
+        k = max(thr, 16 * thr * len(chips) // batch.n_chips)
+        S, Q = sample(chips, k)
+        t = time.perf_counter()
+        oracle_ctypes.detect_batch(batch.chip(chips[0])[0], S, Q, threads=thr)
+        probe_t += time.perf_counter() - t
+        probe_n += k
+    rate = probe_n / probe_t
+    n = int(max(args.cpu_min_pixels, rate * args.cpu_seconds))
+    n = min(n, PIXELS_PER_CHIP * batch.n_chips)
+    el, done, parts = 0.0, 0, []
+    for nobs, chips in sorted(groups.items()):
+        k = min(PIXELS_PER_CHIP * len(chips), -(-n * len(chips) // batch.n_chips))
+        S, Q = sample(chips, k)
+        t = time.perf_counter()
+        oracle_ctypes.detect_batch(batch.chip(chips[0])[0], S, Q, threads=thr)
+        dt = time.perf_counter() - t
+        el += dt
+        done += k
+        parts.append('%d px of %d chips of %d obs (%.1f s)' % (k, len(chips), nobs, dt))
+    out = {'value': done / el, 'unit': 'pixels/s', 'cores': thr, 'kind': 'port',
+           'sample': '%d pixels in the workload\'s cadence mix: %s; pixels strided over each chip; C restatement '
+                     'oracle, OpenMP %d threads, %.1f s in all' % (done, '; '.join(parts), thr, el)}
     out.update(info)
     return out
 
@@ -864,6 +1015,20 @@ def _stop_helpers():
                 k.kill()
         except psutil.Error:
             pass
+    # the record of who else runs as this user right now (not this process, its ancestors or its
+    # children): a process the bench did not start but that a process count at the end would see
+    try:
+        mine = {me.pid} | {p.pid for p in me.parents()}
+        others = []
+        for p in psutil.process_iter(['pid', 'uids', 'cmdline', 'ppid']):
+            if (p.info['pid'] in mine or not p.info['uids'] or p.info['uids'].real != os.getuid()
+                    or not p.info['cmdline']):  # (kernel threads have no command line)
+                continue
+            others.append('%d (ppid %d): %s' % (p.info['pid'], p.info['ppid'], ' '.join(p.info['cmdline'] or [])[:120]))
+        if others:
+            print('bench: other processes of this user at exit: %s' % ' | '.join(others[:12]), file=sys.stderr)
+    except psutil.Error:
+        pass
 
 
 if __name__ == '__main__':

@@ -274,6 +274,12 @@ class EncodingSource(object):
             with self._lock:
                 self._free.append((need, st))
 
+    def close(self):
+        """Drop the free encoded-batch buffers (their pinned memory is released with the last
+        view); batches still handed out keep theirs."""
+        with self._lock:
+            self._free = []
+
 
 # --------------------------------------------------------------------------- the GPU worker
 def _pull_size(queue, batch_chips, tail_chips):
@@ -330,7 +336,7 @@ def _worker(ctx, queue, source, xys, batch_chips, params, width, sink, stats, er
     stop = threading.Event()
     permits = threading.Semaphore(depth + 1)  # one per upload slot
     ft = threading.Thread(target=_fetcher, args=(queue, source, batch_chips, tail_chips, stats, ready, stop, permits),
-                          daemon=True)
+                          daemon=True, name='ccd-fetch-%s' % threading.current_thread().name.rsplit('-', 1)[-1])
     ft.start()
     try:
         clock = time.perf_counter
@@ -508,8 +514,8 @@ def detect_tile(xys, source, queue, device=0, contexts=4, batch_chips=6, params=
     old_aff = bind_to_device_node(device) if bind_numa else None
     try:
         th = [threading.Thread(target=_worker, args=(c, queue, source, xys, int(batch_chips), params, width, sink, stats,
-                                                       errors, int(upload_depth), int(tail_chips)))
-              for c in ctxs]
+                                                       errors, int(upload_depth), int(tail_chips)), name='ccd-worker-%d' % i)
+              for i, c in enumerate(ctxs)]
         for t in th:
             t.start()
         for t in th:

@@ -307,6 +307,10 @@ class TileSource(object):
                 self.allocated += 1
 
     def close(self):
+        """Close the generators and drop the pool chips and free pinned batches."""
         for g in self._gens:
             g.close()
         self._gens = []
+        with self._lock:
+            self._free = []
+            self._pool = None
