@@ -75,14 +75,83 @@ static size_t compact_scalar(const int16_t *src, const uint8_t *keep, const uint
 
 #if defined(__x86_64__)
 #include <immintrin.h>
+/* Streaming writer of one contiguous output range (a block's run of one band): the compressed
+ * values are staged in a small L1-resident buffer laid out like the destination lines, and every
+ * destination line that lies wholly inside the range leaves with a non-temporal store -- no
+ * read-for-ownership of the pinned destination, which costs a DRAM read of every line written
+ * (the encoded batch, ~15 KB per tile pixel, is far larger than the caches).  The range's first
+ * and last lines, which it may share with a neighbouring range (another block, possibly another
+ * thread's), are written with masked ordinary stores of its own elements only. */
+#define NTW_LINES 32
+typedef struct {
+    int16_t stage[(NTW_LINES + 1) * 32] __attribute__((aligned(64)));
+    int16_t *dst; /* destination line of stage[0] (64-byte aligned) */
+    int first;    /* elements of the range's first line below its start (0 once that line is out) */
+    int k;        /* elements staged, counted from stage[0] */
+} ntw_t;
+
+__attribute__((target("avx512f,avx512bw"))) static inline void ntw_begin(ntw_t *w, int16_t *dst) {
+    const uintptr_t a = (uintptr_t)dst;
+    w->dst = (int16_t *)(a & ~(uintptr_t)63);
+    w->first = (int)((a & 63) >> 1);
+    w->k = w->first;
+}
+/* CCDGPU_ENCODE_NT=0: ordinary stores for the full lines too (A/B) */
+static int ntw_stream(void) {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("CCDGPU_ENCODE_NT");
+        v = !(e && *e == '0');
+    }
+    return v;
+}
+__attribute__((target("avx512f,avx512bw"))) static inline void ntw_lines(ntw_t *w, int nl) {
+    const int nt = ntw_stream();
+    for (int i = 0; i < nl; ++i) {
+        const __m512i v = _mm512_load_si512((const void *)(w->stage + 32 * i));
+        if (w->first) {
+            _mm512_mask_storeu_epi16(w->dst, (__mmask32)(0xFFFFFFFFu << w->first), v);
+            w->first = 0;
+        } else if (nt) {
+            _mm512_stream_si512((__m512i *)w->dst, v);
+        } else {
+            _mm512_store_si512((void *)w->dst, v);
+        }
+        w->dst += 32;
+    }
+}
+/* c compressed values (the low lanes of v) onto the range */
+__attribute__((target("avx512f,avx512bw"))) static inline void ntw_put(ntw_t *w, __m512i v, int c) {
+    _mm512_mask_storeu_epi16(w->stage + w->k, (__mmask32)(c == 32 ? 0xFFFFFFFFu : (1u << c) - 1u), v);
+    w->k += c;
+    if (w->k >= NTW_LINES * 32) {
+        const int nl = w->k >> 5;
+        ntw_lines(w, nl);
+        _mm512_store_si512((void *)w->stage, _mm512_load_si512((const void *)(w->stage + 32 * nl)));
+        w->k -= 32 * nl;
+    }
+}
+/* the range is complete: its full lines, then its partial last line */
+__attribute__((target("avx512f,avx512bw"))) static inline void ntw_end(ntw_t *w) {
+    const int nl = w->k >> 5;
+    ntw_lines(w, nl);
+    const int rem = w->k - 32 * nl;
+    if (rem > 0) {
+        const __m512i v = _mm512_load_si512((const void *)(w->stage + 32 * nl));
+        _mm512_mask_storeu_epi16(w->dst, (__mmask32)(((1u << rem) - 1u) & (0xFFFFFFFFu << w->first)), v);
+    }
+    w->first = 0;
+    w->k = 0;
+}
+
 /* the same with AVX-512 VBMI2, 32 observations at a time; m[] = keep bit masks, sm[] = the strict
- * observations' bit masks.  The kept values
- * are compressed in a register and written with a masked store of exactly their count (a
- * compress with a memory destination is microcoded and slow on Zen 4/5). */
+ * observations' bit masks.  The kept values are compressed in a register and appended to the
+ * range's streaming writer (a compress with a memory destination is microcoded and slow on Zen
+ * 4/5). */
 __attribute__((target("avx512f,avx512bw,avx512vbmi2"))) static size_t compact_vbmi2(const int16_t *src,
                                                                                    const uint32_t *m,
                                                                                    const uint32_t *sm, int n,
-                                                                                   int16_t *dst, int *bad) {
+                                                                                   ntw_t *out, int *bad) {
     size_t k = 0;
     int i = 0, w = 0;
     const __m512i fillv = _mm512_set1_epi16(-9999);
@@ -90,8 +159,7 @@ __attribute__((target("avx512f,avx512bw,avx512vbmi2"))) static size_t compact_vb
     for (; i + 32 <= n; i += 32, ++w) {
         const __m512i v = _mm512_loadu_si512((const void *)(src + i));
         const int c = __builtin_popcount(m[w]);
-        _mm512_mask_storeu_epi16(dst + k, (__mmask32)(c == 32 ? 0xFFFFFFFFu : (1u << c) - 1u),
-                                 _mm512_maskz_compress_epi16((__mmask32)m[w], v));
+        ntw_put(out, _mm512_maskz_compress_epi16((__mmask32)m[w], v), c);
         k += (size_t)c;
         nb |= _mm512_mask_cmpneq_epi16_mask((__mmask32)sm[w], v, fillv);
     }
@@ -99,7 +167,7 @@ __attribute__((target("avx512f,avx512bw,avx512vbmi2"))) static size_t compact_vb
         const __mmask32 tail = (__mmask32)((1ull << (n - i)) - 1ull);
         const __m512i v = _mm512_maskz_loadu_epi16(tail, (const void *)(src + i));
         const int c = __builtin_popcount(m[w] & tail);
-        _mm512_mask_storeu_epi16(dst + k, (__mmask32)((1u << c) - 1u), _mm512_maskz_compress_epi16((__mmask32)(m[w] & tail), v));
+        ntw_put(out, _mm512_maskz_compress_epi16((__mmask32)(m[w] & tail), v), c);
         k += (size_t)c;
         nb |= _mm512_mask_cmpneq_epi16_mask((__mmask32)(sm[w] & tail), v, fillv);
     }
@@ -227,6 +295,7 @@ static size_t encode_raw(int32_t n_pix, int32_t n_obs, const int16_t *spectra, c
     memset(sec + 16, 0, 32);
     uint16_t *oq = (uint16_t *)(sec + ENC_HDR);
     int16_t *os = (int16_t *)(sec + ENC_HDR + up(2 * plane, 16));
+    memset((uint8_t *)(oq + plane), 0, up(2 * plane, 16) - 2 * plane);
 #pragma omp parallel for schedule(static) num_threads(nt)
     for (int32_t p = 0; p < n_pix; ++p) {
         memcpy(oq + (size_t)p * n_obs, qa + (size_t)p * n_obs, 2 * (size_t)n_obs);
@@ -335,12 +404,15 @@ static size_t encode_chip(int32_t n_pix, int32_t n_obs, const int16_t *spectra, 
             tot += kept_scratch[p];
         }
         koff[n_pix] = (uint32_t)tot;
+        /* padding after the offsets and after the code rows: deterministic bytes */
+        memset(koff + n_pix + 1, 0, up(4 * ((size_t)n_pix + 1), 16) - 4 * ((size_t)n_pix + 1));
         const size_t bstride = up((size_t)tot, 8);
         h64[0] = (int64_t)tot;
         h64[2] = (int64_t)bstride;
         uint8_t *q4 = sec + ENC_HDR + up(4 * ((size_t)n_pix + 1), 16);
         const size_t rowb = (size_t)(n_obs + 1) / 2;
         int16_t *bands = (int16_t *)(q4 + up((size_t)n_pix * rowb, 16));
+        memset(q4 + (size_t)n_pix * rowb, 0, up((size_t)n_pix * rowb, 16) - (size_t)n_pix * rowb);
         const int vec = have_vbmi2();
         int bad2 = 0, miss = 0;
         /* pass 2: 4-bit QA codes and the kept band values (and the fill observations' values checked).
@@ -355,6 +427,8 @@ static size_t encode_chip(int32_t n_pix, int32_t n_obs, const int16_t *spectra, 
             uint8_t *keep = (uint8_t *)malloc(2 * (size_t)n_obs + 64), *strictm = keep + n_obs + 32;
             uint32_t *km = (uint32_t *)malloc((size_t)mw * 8 * pb), *sm = km + (size_t)mw * pb;
 #if defined(__x86_64__)
+            ntw_t ntw_s; /* (2 KB, 64-byte aligned, on the thread's stack) */
+            ntw_t *ntw = &ntw_s;
             if (vec) {
 #pragma omp for schedule(static)
                 for (int32_t p0 = 0; p0 < n_pix; p0 += pb) {
@@ -365,10 +439,12 @@ static size_t encode_chip(int32_t n_pix, int32_t n_obs, const int16_t *spectra, 
                     if (miss) continue;  /* the chip is encoded again */
                     for (int b = 0; b < 7; ++b) {
                         const int16_t *src = spectra + (size_t)b * plane;
-                        int16_t *dst = bands + (size_t)b * bstride;
+                        /* the block's run of band b is one contiguous range (koff[p0] .. koff[pe]) */
+                        ntw_begin(ntw, bands + (size_t)b * bstride + koff[p0]);
                         for (int32_t p = p0; p < pe; ++p)
                             compact_vbmi2(src + (size_t)p * n_obs, km + (size_t)(p - p0) * mw, sm + (size_t)(p - p0) * mw,
-                                          n_obs, dst + koff[p], &bad2);
+                                          n_obs, ntw, &bad2);
+                        ntw_end(ntw);
                     }
                 }
             } else
@@ -401,6 +477,9 @@ static size_t encode_chip(int32_t n_pix, int32_t n_obs, const int16_t *spectra, 
                     compact_scalar(spectra + (size_t)b * plane + (size_t)p * n_obs, keep, strictm, n_obs,
                                    bands + (size_t)b * bstride + koff[p], &bad2);
             }
+#if defined(__x86_64__)
+            if (vec) _mm_sfence();  /* the streamed lines are visible before the batch is uploaded */
+#endif
             free(keep);
             free(km);
         }
@@ -437,6 +516,7 @@ int64_t ccdgpu_encode_chips(int32_t n_chips, const int32_t *n_pix, const int32_t
     uint32_t *kept = (uint32_t *)malloc(4 * (size_t)maxp);
     if (!kept) return -3;
     size_t pos = table_bytes(n_chips);
+    memset(out + 8 + 16 * ((size_t)n_chips + 1), 0, pos - (8 + 16 * ((size_t)n_chips + 1)));  /* table padding */
     int64_t pbase = 0, dbase = 0;
     for (int32_t c = 0; c < n_chips; ++c) {
         off[c] = (int64_t)pos;
@@ -447,6 +527,7 @@ int64_t ccdgpu_encode_chips(int32_t n_chips, const int32_t *n_pix, const int32_t
             free(kept);
             return -3;
         }
+        memset(out + pos + sz, 0, up(sz, ENC_ALIGN) - sz);  /* section padding */
         pos += up(sz, ENC_ALIGN);
         pbase += n_pix[c];
         dbase += (int64_t)n_pix[c] * n_obs[c];
