@@ -2705,6 +2705,8 @@ __device__ __forceinline__ void coop_comp(const Px &P, int fa, int nf, int dref,
     // numpy's choice among the ties (lane j < need: the sorted index of the j-th one taken)
     const bool qs = T > need && !ARGS().p.argsort_stable;
     const int tk = qs ? qs_ties(P, fa, nf, dref, less) : -1;
+    PH_COUNT(P, 22, E > W ? 1 : 0)     // (diagnostic build) selections of more entries than a wave
+    PH_COUNT(P, 23, T > need ? 1 : 0)  // ... and with more ties at the cut-off than still needed
     double acc[NB];  // per band (detection bands only)
 #pragma unroll
     for (int b = 0; b < NB; ++b) acc[b] = 0.0;

@@ -216,6 +216,40 @@ def tie_years_case():
     return _TIE_YEARS
 
 
+def tie_cycles_case():
+    """find_closest_doy with more tied entries than a wave holds: 30 four-year cycles of the same
+    40 dates 16 days apart (120 years, 1200 observations, descending).  Every date shares its
+    day-of-4-years bin with its copies in the other cycles, so once a fit window spans ~22 of
+    them the reference date's own bin holds fewer than 24 entries and the two bins 16 days away
+    hold ~22 each: the entries at the cut-off distance number more than 40 and the selection
+    more than 64 -- coop_comp's multi-chunk loop, and with ARGSORT='stable' its rank from reloaded
+    bucket records.  The kernel needs the exact comparison rmse only for steps its bounds leave
+    open, i.e. where the comparison rmse is well above the variogram: the pixels carry a 7-year
+    oscillation of amplitude 100 (smooth: a small variogram, residuals about the harmonic model
+    well above it) and 5 % clear spikes of 200-600.  Measured with the diagnostic build
+    (tools/coop_ties.py): 63 exact comparison rmse steps on these 8 pixels, 56 with more ties
+    at the cut-off than needed, 2 selecting more than 64 entries."""
+    d = np.concatenate([693600 + 1461 * c + 16 * np.arange(40) for c in range(30)]).astype(np.int64)
+    n = d.shape[0]
+    w = 2 * np.pi / 365.2425
+    base = np.array([500, 800, 700, 2800, 2000, 1200, 2950.])
+    amp = np.array([150, 200, 250, 600, 400, 300, 0.])
+    S, Q = [], []
+    for k in range(8):
+        rng = np.random.default_rng(5000 + k)
+        y = base[:, None] + amp[:, None] * np.cos(w * d[None, :] + rng.uniform(0, 2 * np.pi, (7, 1))) + rng.normal(0, 8, (7, n))
+        y[:6] += 100 * np.sin(2 * np.pi * d[None, :] / (7 * 365.25) + rng.uniform(0, 2 * np.pi, (6, 1)))
+        sp = rng.uniform(size=n) < 0.05
+        y[:6, sp] += rng.choice([-1, 1], size=(6, sp.sum())) * rng.uniform(200, 600, (6, sp.sum()))
+        y[6] = base[6] + rng.normal(0, 20, n)
+        y[:6] = np.clip(y[:6], 20, 9900)
+        S.append(np.round(y).astype(np.int16))
+        Q.append(np.full(n, 66, np.uint16))
+    s = np.stack(S, axis=1)
+    q = np.stack(Q, axis=0)
+    return d[::-1].copy(), s[:, :, ::-1].copy(), q[:, ::-1].copy()
+
+
 def main():
     only = set(sys.argv[1:])
     cases = {
@@ -232,6 +266,8 @@ def main():
     cases['tie_years'] = (tie_years_case(), None)
     cases['tie_years_stable'] = (tie_years_case(), {'ARGSORT': 'stable'})
     cases['dup_shuffled_stable'] = (cases['dup_shuffled'][0], {'ARGSORT': 'stable'})
+    cases['tie_cycles'] = (tie_cycles_case(), None)
+    cases['tie_cycles_stable'] = (tie_cycles_case(), {'ARGSORT': 'stable'})
     with multiprocessing.Pool(min(8, os.cpu_count() or 1)) as pool:
         for name, ((d, s, q), params) in cases.items():
             if only and name not in only:
