@@ -97,7 +97,8 @@ typedef struct ccdgpu_result {
     int32_t mask_words;         /* (n_obs + 31) / 32                                      */
     int32_t *procedure;         /* [n_pix] CCDGPU_PROC_*                                  */
     double *probs;              /* [n_pix][3] cloud, snow, water                          */
-    int64_t *sorted_dates;      /* [n_obs] ascending (stable argsort of the input dates)  */
+    int64_t *sorted_dates;      /* [n_obs] ascending (argsort of the input dates, ties in */
+                                /* params.argsort_stable's order)                         */
     int32_t *sort_index;        /* [n_obs] input position of each sorted observation      */
     int32_t error_pixel;        /* first pixel with an unsupported QA value, else -1      */
     double seconds_kernel;      /* device time of the detection kernels (HIP events)      */
