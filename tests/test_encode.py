@@ -211,3 +211,19 @@ def test_encoded_check_rejects_malformed_batches_on_the_host():
     corrupt(lambda b: h64(b, 0).__setitem__(slice(0, 3, 2), [64 * 1421 * 2, 64 * 1421 * 2]))
     corrupt(lambda b: setattr(b, 'nbytes_encoded', off[2] - 64))
     corrupt(lambda b: b.buf[off[1] + 4:off[1] + 8].view(np.int32).__setitem__(0, 41))
+
+
+@pytest.mark.parametrize('nt', ['1', '0'])
+def test_streaming_writer_fills_exactly_its_range(tmp_path, nt):
+    """The encoder's streaming writer (ntw_*: band runs staged in L1, full lines out with
+    non-temporal stores, the ranges' shared first / last lines with masked ordinary stores) on
+    400 random ranges -- any start alignment, 0..32 values per append -- writes every value of its
+    range and nothing outside it (tests/native/ntw_check.c; AVX-512F/BW, no VBMI2 needed)."""
+    exe = str(tmp_path / 'ntw_check')
+    subprocess.run(['gcc', '-O2', '-fopenmp', '-I', os.path.join(ROOT, 'include'), '-o', exe,
+                    os.path.join(HERE, 'native', 'ntw_check.c')], check=True)
+    out = subprocess.run([exe], env=dict(os.environ, CCDGPU_ENCODE_NT=nt), capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    if out.stdout.startswith('skip'):
+        pytest.skip(out.stdout.strip())
+    assert out.stdout.strip() == 'ok'
