@@ -540,6 +540,7 @@ class _ThreadCpu(object):
         import threading
         names = {t.native_id: t.name for t in threading.enumerate() if getattr(t, 'native_id', None)}
         base = '/proc/self/task'
+        initial = not self._last  # the first sample: every thread alive now counts from here
         for tid in os.listdir(base):
             try:
                 with open('%s/%s/stat' % (base, tid)) as f:
@@ -550,7 +551,7 @@ class _ThreadCpu(object):
             f = txt[txt.rindex(')') + 2:].split()
             cpu = (int(f[11]) + int(f[12])) / self._tick  # utime + stime
             t = int(tid)
-            self._first.setdefault(t, cpu if not self._last else 0.0)
+            self._first.setdefault(t, cpu if initial else 0.0)
             self._last[t] = cpu
             self._names[t] = names.get(t, self._names.get(t, comm))
 
