@@ -49,8 +49,13 @@ def get_in(keys, coll, default=None):
         return default
 
 
+_NATIVE = frozenset((int, float, str, bool, type(None)))
+
+
 def denumpify(arg):
-    """merlin.functions.denumpify: numpy scalars/arrays -> native Python, containers kept."""
+    """merlin.functions.denumpify: numpy scalars/arrays -> native Python, containers kept.  A list
+    or tuple of native scalars (a row's ISO dates, its mask) is copied in one pass instead of one
+    recursive call per element -- the same result."""
     if isinstance(arg, np.generic):
         return arg.item()
     if isinstance(arg, np.ndarray):
@@ -58,10 +63,33 @@ def denumpify(arg):
     if isinstance(arg, dict):
         return {k: denumpify(v) for k, v in arg.items()}
     if isinstance(arg, list):
+        if _NATIVE.issuperset(map(type, arg)):
+            return list(arg)
         return [denumpify(v) for v in arg]
     if isinstance(arg, tuple):
+        if _NATIVE.issuperset(map(type, arg)):
+            return tuple(arg)
         return tuple(denumpify(v) for v in arg)
     return arg
+
+
+_iso_memo = {}
+
+
+def _iso_dates(dates):
+    """[date.fromordinal(o).isoformat() for o in dates] as a new list, the strings of a date
+    vector built once: a chip's pixels (and a partition's records of one chip) share it, and the
+    conversion is most of a row's formatting time otherwise."""
+    if not isinstance(dates, (list, tuple, np.ndarray)):
+        dates = list(dates)  # (an iterator: one pass for the key, one for the strings)
+    key = tuple(dates)
+    iso = _iso_memo.get(key)
+    if iso is None:
+        iso = [date.fromordinal(o).isoformat() for o in dates]
+        if len(_iso_memo) >= 16:
+            _iso_memo.clear()
+        _iso_memo[key] = iso
+    return list(iso)
 
 
 # ---- reference API ------------------------------------------------------------------------------
@@ -137,7 +165,7 @@ def default(change_models):
 def format(cx, cy, px, py, dates, ccdresult):
     """One row dict per change model (pyccd.py:106-148).  ``dates`` in input order, ``mask`` in
     pyccd's sorted-date order, exactly as the reference emits them."""
-    return [denumpify(
+    rows = [denumpify(
         {'cx': cx,
          'cy': cy,
          'px': px,
@@ -175,9 +203,12 @@ def format(cx, cy, px, py, dates, ccdresult):
          's1int': get_in(['swir1', 'intercept'], cm, None),
          's2int': get_in(['swir2', 'intercept'], cm, None),
          'thint': get_in(['thermal', 'intercept'], cm, None),
-         'dates': [date.fromordinal(o).isoformat() for o in dates],
+         'dates': None,  # (set below: built here, native already)
          'mask': get('processing_mask', ccdresult, None)})
         for cm in default(get('change_models', ccdresult, None))]
+    for row in rows:
+        row['dates'] = _iso_dates(dates)
+    return rows
 
 
 def detect(timeseries):

@@ -253,7 +253,7 @@ def pixel_result(u, px, algorithm):
     a, b = int(u.seg_offsets[px]), int(u.seg_offsets[px + 1])
     probs = u.probs[px]
     return {'algorithm': algorithm,
-            'processing_mask': [int(x) for x in u.mask[px]],
+            'processing_mask': np.asarray(u.mask[px]).astype(np.int64).tolist(),  # (Python ints)
             'procedure': PROCEDURES[int(u.procedure[px])],
             'change_models': [segment_to_change_model(s) for s in u.segments[a:b]],
             'cloud_prob': float(probs[0]), 'snow_prob': float(probs[1]),
