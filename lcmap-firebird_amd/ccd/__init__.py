@@ -92,12 +92,28 @@ def detect_records(records, params=None):
     """[(key, {dates, blues..thermals, qas}), ...] -> [(key, result), ...].  Records are grouped
     by date vector (a chip's pixels, as merlin.create builds them) and every group of the call
     runs in one device launch (detect_groups)."""
+    # group by date vector: a record's list is compared with each group's first one (a C-level
+    # list comparison) under a cheap (length, first, last) key, so a record's dates are converted
+    # to an array only when they open a group (merlin's records carry the dates as a list)
     groups = {}
+    order = []
     for idx, (key, rec) in enumerate(records):
-        d = np.asarray(rec['dates'], dtype=np.int64)
-        groups.setdefault(d.tobytes(), (d, []))[1].append((idx, key, rec))
+        dl = rec['dates']
+        if isinstance(dl, np.ndarray):
+            k = ('a', np.asarray(dl, dtype=np.int64).tobytes())
+        else:
+            dl = dl if isinstance(dl, list) else list(dl)
+            k = (len(dl), dl[0] if dl else None, dl[-1] if dl else None)
+        for g in groups.setdefault(k, []):
+            if k[0] == 'a' or g[0] is dl or g[0] == dl:
+                g[2].append((idx, key, rec))
+                break
+        else:
+            g = (dl, np.asarray(dl, dtype=np.int64), [(idx, key, rec)])
+            groups[k].append(g)
+            order.append(g)
     arrays, members_of = [], []
-    for d, members in groups.values():
+    for _, d, members in order:
         n = d.shape[0]
         spectra = np.empty((7, len(members), n), dtype=np.int16)
         qas = np.empty((len(members), n), dtype=np.uint16)
