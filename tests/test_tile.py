@@ -327,3 +327,52 @@ def test_rows_copy_size_is_learned_and_an_overflow_still_returns_every_row():
     off, rows, _ = ctx.run_slot_end_rows()
     assert ctx.overflowed == before + 1
     assert rows.tobytes() == ref[1][1].tobytes()
+
+
+@pytest.mark.parametrize('threads', [0, 2])
+def test_parquet_sink_writes_the_reference_tables(tmp_path, threads):
+    """ccdc.runner.ParquetSink through the tile driver (oracle-backed contexts): one segment /
+    pixel / chip file per chip with the reference schemas' columns and Arrow storage types, the
+    segment rows equal to the rows the run handed the sink, the pixel masks to its mask bits --
+    written inline or on a pool of writer threads from copies of the reused buffers."""
+    import pyarrow.parquet as pq
+    from ccdc import runner, sink as sink_mod
+    from ccdc import segment as seg_mod, pixel as pix_mod, chip as chip_mod
+    from ccdgpu import abi
+    from rows_util import OracleContext
+    n = 4
+    ref = runner.SummarySink(keep_rows=True)
+    runner.changedetection(tile(), source, contexts=1, batch_chips=2, number=n, sink=ref,
+                           context_factory=lambda dev: OracleContext(dev, threads=2))
+    ps = runner.ParquetSink(str(tmp_path), threads=threads)
+    res = runner.changedetection(tile(), source, contexts=2, batch_chips=2, number=n, sink=ps,
+                                 context_factory=lambda dev: OracleContext(dev, threads=2))
+    ps.close()
+    assert [c['pos'] for c in res['chips']] == list(range(n))
+    for pos, (cx, cy) in enumerate(res['xys']):
+        off, rows, mask = ref.rows[pos]
+        seg = pq.read_table(str(tmp_path / 'segment' / ('%d_%d.parquet' % (cx, cy))))
+        pix = pq.read_table(str(tmp_path / 'pixel' / ('%d_%d.parquet' % (cx, cy))))
+        chp = pq.read_table(str(tmp_path / 'chip' / ('%d_%d.parquet' % (cx, cy))))
+        assert seg.schema.equals(sink_mod.arrow_schema(seg_mod.schema()))
+        assert pix.schema.equals(sink_mod.arrow_schema(pix_mod.schema()))
+        assert chp.schema.equals(sink_mod.arrow_schema(chip_mod.schema()))
+        assert seg.equals(sink_mod.segment_table(cx, cy, rows))
+        assert seg.num_rows == rows.shape[0]
+        got_mask = np.array(pix.column('mask').to_pylist(), dtype=np.int8)
+        assert np.array_equal(got_mask, np.asarray(mask, dtype=np.int8))
+        assert chp.column('dates').to_pylist()[0] == sink_mod.iso_days(source([pos]).chip(0)[0]).tolist()
+
+
+def test_parquet_sink_write_error_reaches_the_caller(tmp_path):
+    """A background write that fails (here: the output directory is a file) is raised by the
+    tile driver, not lost in the writer pool."""
+    from ccdc import runner
+    from rows_util import OracleContext
+    bad = tmp_path / 'not_a_dir'
+    bad.write_text('x')
+    ps = runner.ParquetSink(str(bad), threads=2)
+    with pytest.raises(Exception):
+        runner.changedetection(tile(), source, contexts=1, batch_chips=2, number=2, sink=ps,
+                               context_factory=lambda dev: OracleContext(dev, threads=2))
+    ps.close()  # (the failed write was raised above; nothing left pending)
