@@ -666,7 +666,7 @@ int ccdgpu_stage_chipmunk(ccdgpu_ctx *c, const ccdgpu_params *params, int32_t n_
     int rc = make_shape(n_chips, np.data(), no.data(), sh);
     if (rc) return rc;
     if ((rc = stage_alloc(c, params, sh, dates))) return rc;
-    if ((rc = c->b64.ensure((size_t)text_bytes + 1)) || (rc = c->b64_off.ensure((size_t)n_off))) return rc;
+    if ((rc = c->b64.ensure((size_t)text_bytes + 8)) || (rc = c->b64_off.ensure((size_t)n_off))) return rc;
     HIPCHK(hipMemcpyAsync(c->b64.p, text, (size_t)text_bytes, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->b64_off.p, text_offsets, sizeof(int64_t) * (size_t)n_off, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemsetAsync(c->counters.p, 0, sizeof(unsigned long long) * 8, c->stream));

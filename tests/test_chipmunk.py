@@ -98,6 +98,31 @@ def test_device_unpack_matches_host_restatement():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('n_pix,n_obs', [(97, 131), (10000, 257)])
+def test_device_unpack_unaligned_payloads(n_pix, n_obs):
+    """Payloads at every offset mod 4 (the kernel's 32-bit quantum loads fall back to bytes),
+    with '#' between them (never decoded), odd pixel counts ('=' padding) and partial tiles."""
+    import ccdgpu
+    ctx = ccdgpu.Context(0)
+    dates, spectra, qa, chips = synthetic(n_pix=n_pix, n_obs=n_obs, seed=5)
+    d, text, offsets = chipmunk.pack_text([chipmunk.group(chips)[(-1815585, 1064805)]])
+    enc = 4 * ((2 * n_pix + 2) // 3)
+    out, shifted = bytearray(), np.full_like(offsets, -1)
+    for i, (o, l) in enumerate(np.ndindex(*offsets.shape[1:])):
+        if offsets[0, o, l] < 0:
+            continue
+        out += b'#' * (i % 4)
+        shifted[0, o, l] = len(out)
+        out += text[offsets[0, o, l]:offsets[0, o, l] + enc]
+    shifted[0, 3, 1] = -1
+    ctx.stage_chipmunk(d, bytes(out), shifted, n_pix)
+    es, eq = chipmunk_ref.decode(d, bytes(out), shifted, n_pix)
+    got_s, got_q = ctx.staged_inputs()
+    assert np.array_equal(got_s, es) and np.array_equal(got_q, eq)
+    ctx.close()
+
+
+@pytest.mark.gpu
 def test_device_unpack_rejects_bad_base64():
     import ccdgpu
     ctx = ccdgpu.Context(0)
