@@ -98,10 +98,11 @@ def test_device_unpack_matches_host_restatement():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('n_pix,n_obs', [(97, 131), (10000, 257)])
+@pytest.mark.parametrize('n_pix,n_obs', [(97, 131), (98, 129), (10000, 257)])
 def test_device_unpack_unaligned_payloads(n_pix, n_obs):
-    """Payloads at every offset mod 4 (the kernel's 32-bit quantum loads fall back to bytes),
-    with '#' between them (never decoded), odd pixel counts ('=' padding) and partial tiles."""
+    """Payloads at every offset mod 4 (the kernel's 8-character loads are then unaligned), with
+    '#' between them (never decoded), '=' and '==' padding (97 / 98 pixels) and partial tiles
+    of both dimensions."""
     import ccdgpu
     ctx = ccdgpu.Context(0)
     dates, spectra, qa, chips = synthetic(n_pix=n_pix, n_obs=n_obs, seed=5)
@@ -134,6 +135,11 @@ def test_device_unpack_rejects_bad_base64():
         ctx.stage_chipmunk(d, bytes(bad), offsets, 50)
     with pytest.raises(ccdgpu.CcdGpuError):  # payload past the end of the text
         ctx.stage_chipmunk(d, text[:-10], offsets, 50)
+    pad = bytearray(text)
+    pad[offsets[0, 1, 7] + 8] = ord('=')  # padding in the first place of a quantum
+    with pytest.raises(ccdgpu.CcdGpuError):
+        ctx.stage_chipmunk(d, bytes(pad), offsets, 50)
+    ctx.stage_chipmunk(d, text, offsets, 50)  # the context still stages a good text afterwards
     ctx.close()
 
 
