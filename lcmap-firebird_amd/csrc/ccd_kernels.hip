@@ -777,7 +777,10 @@ __device__ __forceinline__ void gmax8f2(float u, float v, float &ru, float &rv X
 // update reads it directly.  A change d of w_J moves h_k by -G_kJ d for k != J and leaves h_J as
 // it is (the G_JJ terms cancel), so the broadcast column carries a zero on its diagonal.
 // Per coordinate: soft threshold (3 VALU), d (1 fused), lane J's w (1, exec-masked), 2 DPP FMAs.
-template <int J>
+// HALF: 0 = both band groups of each 16-lane row take the broadcast; 1 / 2 = only the even (lanes
+// 0-7 of the row) / odd (lanes 8-15) groups are live, so the other group's FMA (which would add
+// zeros to a finished group) is left out.
+template <int J, int HALF = 0>
 __device__ __forceinline__ void cd_coord(unsigned long long mJ /* live lanes of coordinate J */,
                                          double alpha, double rgkk, double ngcolJ, double &h, double &w XL) {
     EXEC_FULL();
@@ -800,11 +803,34 @@ __device__ __forceinline__ void cd_coord(unsigned long long mJ /* live lanes of 
     // lane J, lanes 8-15 lane 8 + J.  s_nop 1 before each: a DPP FMA reads its operands (the
     // accumulator included) 2 wait states behind a VALU write of them -- back to back, the second
     // FMA loses the first one's result (tools/probe/dpp64.hip, measured on gfx950).
-    asm volatile("s_nop 1\n\t"
-                 "v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0x3\n\t"
-                 "s_nop 1\n\t"
-                 "v_fmac_f64_dpp %0, %1, %2 row_newbcast:%4 row_mask:0xf bank_mask:0xc"
-                 : "+v"(h) : "v"(d), "v"(ngcolJ), "i"(J), "i"(J + 8));
+    if (HALF == 0)
+        asm volatile("s_nop 1\n\t"
+                     "v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0x3\n\t"
+                     "s_nop 1\n\t"
+                     "v_fmac_f64_dpp %0, %1, %2 row_newbcast:%4 row_mask:0xf bank_mask:0xc"
+                     : "+v"(h) : "v"(d), "v"(ngcolJ), "i"(J), "i"(J + 8));
+    else if (HALF == 1)
+        asm volatile("s_nop 1\n\t"
+                     "v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0x3"
+                     : "+v"(h) : "v"(d), "v"(ngcolJ), "i"(J));
+    else
+        asm volatile("s_nop 1\n\t"
+                     "v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xc"
+                     : "+v"(h) : "v"(d), "v"(ngcolJ), "i"(J + 8));
+}
+
+// one cyclic sweep over the PC active coordinates (pc at run time when PC = 0)
+template <int PC, int HALF>
+__device__ __forceinline__ void cd_coords(int pc, unsigned long long lm, double alpha, double rgkk,
+                                          const double (&gcol)[7], double &h, double &w XL) {
+    constexpr unsigned long long COL = 0x0001010101010101ull;  // coordinate J's lanes (b, J): one bit per group
+    cd_coord<0, HALF>(lm & COL, alpha, rgkk, gcol[0], h, w);
+    if (pc > 1) cd_coord<1, HALF>(lm & (COL << 1), alpha, rgkk, gcol[1], h, w);
+    if (pc > 2) cd_coord<2, HALF>(lm & (COL << 2), alpha, rgkk, gcol[2], h, w);
+    if (pc > 3) cd_coord<3, HALF>(lm & (COL << 3), alpha, rgkk, gcol[3], h, w);
+    if (pc > 4) cd_coord<4, HALF>(lm & (COL << 4), alpha, rgkk, gcol[4], h, w);
+    if (pc > 5) cd_coord<5, HALF>(lm & (COL << 5), alpha, rgkk, gcol[5], h, w);
+    if (pc > 6) cd_coord<6, HALF>(lm & (COL << 6), alpha, rgkk, gcol[6], h, w);
 }
 
 // sklearn 0.18 enet_coordinate_descent (beta = 0, cyclic, duality-gap stop) in gradient form,
@@ -830,8 +856,6 @@ __device__ __forceinline__ int cd_sweep(Lds *L, int pc_rt, double alpha, int max
     const double tol_m = -0x1p-45 * tol;  // exact (a power of two)
     const float tol_f = (float)tol;
     const bool can = act && gkk != 0.0;  // sklearn skips zero-norm columns
-    // coordinate J's lanes (b, J), b < 7: one bit per band group
-    constexpr unsigned long long COL = 0x0001010101010101ull;
     double w = 0.0, h = q;  // h = g + G_kk w = q at w = 0
     // loop control in wave-uniform lane masks (SALU): finished groups (all 8 lanes of a band
     // whose duality gap met tol, and lanes 56-63), and the lanes sklearn updates at all
@@ -870,13 +894,10 @@ __device__ __forceinline__ int cd_sweep(Lds *L, int pc_rt, double alpha, int max
 #endif
         const unsigned long long lm = cmask & ~dmask;  // live lanes (all coordinates)
         const double w0 = w;
-        cd_coord<0>(lm & COL, alpha, rgkk, gcol[0], h, w);
-        if (pc > 1) cd_coord<1>(lm & (COL << 1), alpha, rgkk, gcol[1], h, w);
-        if (pc > 2) cd_coord<2>(lm & (COL << 2), alpha, rgkk, gcol[2], h, w);
-        if (pc > 3) cd_coord<3>(lm & (COL << 3), alpha, rgkk, gcol[3], h, w);
-        if (pc > 4) cd_coord<4>(lm & (COL << 4), alpha, rgkk, gcol[4], h, w);
-        if (pc > 5) cd_coord<5>(lm & (COL << 5), alpha, rgkk, gcol[5], h, w);
-        if (pc > 6) cd_coord<6>(lm & (COL << 6), alpha, rgkk, gcol[6], h, w);
+        // (one sweep body for every live-group pattern: a second body for live groups all in one
+        // half of their rows -- one broadcast FMA per coordinate, 36 % of C3 sweeps -- measured 5 %
+        // slower, profiles/r06/ab/half_row_skip_*)
+        cd_coords<PC, 0>(pc, lm, alpha, rgkk, gcol, h, w);
         // every coordinate moves once per sweep: d_w_ii = |w_new - w_old| of the lane's own one.
         // sklearn's d_w_max / w_max < tol (w_max = 0 is the check's own first clause), decided
         // first on the float32 roundings of the two maxima (max commutes with the monotone
@@ -897,6 +918,9 @@ __device__ __forceinline__ int cd_sweep(Lds *L, int pc_rt, double alpha, int max
             const unsigned long long gem = wokm & bal(D > tw * (1.0f + 0x1p-16f));
             rl = ltm;
             const unsigned long long ambm = ~dmask & ~ltm & ~gem;
+#ifdef CCD_CD_CHKSTAT
+            PH_COUNT(P, 27, ambm ? 1 : 0)
+#endif
             if (ambm) {
                 const double d_w_max = gmax8(fabs(w - w0));
                 const double w_max = gmax8(fabs(w));
@@ -912,6 +936,19 @@ __device__ __forceinline__ int cd_sweep(Lds *L, int pc_rt, double alpha, int max
             }
         }
         const unsigned long long chk = ~dmask & (wz | rl | (it == max_iter - 1 ? ~0ull : 0ull));
+#ifdef CCD_CD_CHKSTAT
+        {
+            // diagnostic: sweeps, sweeps that take the duality-gap test, sweeps whose live band
+            // groups all sit in one half of their 16-lane rows (even groups 0, 2, 4, 6 or odd 1, 3, 5:
+            // one of the two broadcast FMAs would do); slot 27: sweeps whose float pre-check of the
+            // stopping ratio is ambiguous (the 64-bit reductions)
+            constexpr unsigned long long EVEN = 0x00FF00FF00FF00FFull;
+            const unsigned long long live = ~dmask;
+            PH_COUNT(P, 24, 1)
+            PH_COUNT(P, 25, chk ? 1 : 0)
+            PH_COUNT(P, 26, ((live & EVEN) == 0ull || (live & ~EVEN) == 0ull) ? 1 : 0)
+        }
+#endif
         if (chk) {
             const double xta = act ? fma(-gkk, w, h) : 0.0;  // X^T R = g = h - G_kk w
             const double dual = gmax8(fabs(xta));
@@ -3506,7 +3543,7 @@ __device__ __forceinline__ void lookforward(Px &P, int &wa, int &wb) {
         stat_uniform(ST_FLOPS, (unsigned long long)ne *
                 ((unsigned long long)k * (7 * 2 * 8 + 5 * 3) + (unsigned long long)nf * 6 + 5 * 48));
         PH_COUNT(P, 16, ne)
-#ifndef CCD_CD_CYCLES  // (slots 24-27 carry the coordinate-descent cycle statistics there)
+#if !defined(CCD_CD_CYCLES) && !defined(CCD_CD_CHKSTAT)  // (slots 24-27 carry the coordinate-descent statistics there)
         PH_COUNT(P, 24, ne <= 16 ? 1 : 0)
         PH_COUNT(P, 25, ne <= 32 ? 1 : 0)
         PH_COUNT(P, 26, nv)

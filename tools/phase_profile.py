@@ -49,6 +49,17 @@ if os.environ.get('CCD_DIAG_LIB', '').endswith('cdcyc.so'):
     out['cd groups at max_iter that cycled'] = c
     out['mean detection sweep'] = it / c if c else None
     out['mean period'] = per / c if c else None
+if os.environ.get('CCD_DIAG_LIB', '').endswith('cdchk.so'):
+    # CCD_CD_CHKSTAT build: slots 24-27 = coordinate-descent wave sweeps (cd_sweep), those that take
+    # the duality-gap test, those whose live band groups sit in one half of their 16-lane rows,
+    # those whose float pre-check of the stopping ratio was ambiguous
+    for i, n in enumerate(['batches ne<=16', 'batches ne<=32', 'batch valid lanes', 'batches without terminal step']):
+        out.pop(n, None)
+    sw = dc[8 + 24] or 1
+    out['cd wave sweeps'] = dc[8 + 24]
+    out['cd sweeps with gap test'] = dc[8 + 25] / sw
+    out['cd sweeps with live groups in one row half'] = dc[8 + 26] / sw
+    out['cd sweeps with ambiguous ratio pre-check'] = dc[8 + 27] / sw
 out['pixels'] = chips * 10000
 out['cycles_per_pixel'] = tot / out['pixels']
 print(json.dumps(out, indent=1))
