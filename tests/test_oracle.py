@@ -145,3 +145,51 @@ def test_pairwise_sum_is_numpys():
     for n in list(range(0, 40)) + [127, 128, 129, 300, 1000]:
         a = rng.standard_normal(n) ** 2 * 10.0 ** rng.integers(-3, 6, n)
         assert lib.ccdoracle_np_pairwise_sum(np.ascontiguousarray(a).ctypes.data, n) == float(np.sum(a))
+
+
+def _unpacked_bytes(u):
+    return [np.ascontiguousarray(getattr(u, k)).tobytes() for k in ('segments', 'seg_offsets', 'mask', 'procedure', 'probs')]
+
+
+def test_restatements_never_read_band_values_of_fill_cloud_shadow_observations():
+    """The runner's default 'unread' transport encoding (ccdgpu.unread_drop_bits) sends no band
+    values for observations whose QA has the fill, cloud or shadow bit, on the premise that no
+    procedure reads them (qabitval classes them fill / cloud / shadow whatever else is set, and
+    the standard, permanent-snow and insufficient-clear filters keep none of those classes).  Both
+    restatements give the same results -- every segment field, mask, procedure and probability,
+    bit for bit -- when those band values are replaced by random int16 values: on C2-C5 chips
+    (standard and insufficient-clear pixels) and the mixed_edge golden's pixels (all three
+    procedures) with the C oracle, and on pixels of each procedure with the numpy restatement
+    (pyccd's module structure)."""
+    import ccdgpu
+    drop, _ = ccdgpu.unread_drop_bits(None)
+    assert drop
+    rng = np.random.default_rng(6)
+    procs = set()
+    cases = [(synth.chip(synth.config(cfg), chip, 0, npx), None, nref)
+             for cfg, chip, npx, nref in ((3, 1, 120, 2), (4, 2, 200, 4), (5, 3, 80, 1), (2, 4, 120, 2))]
+    inputs, params, _ = golden_util.load('mixed_edge')
+    cases.append((inputs, params, 6))
+    for (d, s, q), params, nref in cases:
+        gone = (q & drop) != 0
+        assert gone.any() and not gone.all()
+        s2 = s.copy()
+        s2[:, gone] = rng.integers(-32768, 32768, size=(7, int(gone.sum())), dtype=np.int16)
+        rc0, u0 = oracle_ctypes.detect_batch(d, s, q, params=params, threads=4)
+        rc1, u1 = oracle_ctypes.detect_batch(d, s2, q, params=params, threads=4)
+        assert rc0 == 0 and rc1 == 0
+        assert _unpacked_bytes(u0) == _unpacked_bytes(u1)
+        procs |= set(int(x) for x in np.asarray(u0.procedure))
+        # the numpy restatement on the pixels of each procedure the chip has (at most nref each)
+        pick = []
+        for pr in sorted(set(int(x) for x in np.asarray(u0.procedure))):
+            pick += [int(i) for i in np.flatnonzero(np.asarray(u0.procedure) == pr)[:nref]]
+        for px in pick:
+            with warnings.catch_warnings():
+                warnings.simplefilter('ignore')
+                r0 = ccd_ref.detect(d, *[s[b, px] for b in range(7)], q[px], params=params)
+                r1 = ccd_ref.detect(d, *[s2[b, px] for b in range(7)], q[px], params=params)
+            assert r0['procedure'] == r1['procedure']
+            assert list(r0['processing_mask']) == list(r1['processing_mask'])
+            assert repr(r0['change_models']) == repr(r1['change_models'])
+    assert len(procs) == 3, procs
