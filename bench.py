@@ -93,9 +93,10 @@ def parse():
                          '(strong scaling; value = the tile\'s pixels / its wall time) instead of one tile per rank')
     ap.add_argument('--no-north-star', action='store_true',
                     help='N > 1: skip the extra one-tile-over-all-ranks run reported as north_star_tile')
-    ap.add_argument('--tile-parity-pixels', type=int, default=4,
+    ap.add_argument('--tile-parity-pixels', type=int, default=16,
                     help='pixels per tile position re-detected by the C oracle after the timed tile run '
-                         '(tile.parity_sample: 4 x 2500 = 10^4 pixels per tile, ~12 s of oracle time; 0 = none)')
+                         '(tile.parity_sample: 16 x 2500 = 4 x 10^4 pixels per tile, ~14 s of oracle time on 16 '
+                         'threads; 0 = none)')
     ap.add_argument('--roofline-launches', type=int, default=3,
                     help='single-context launches of the resident batch timed for the roofline (per-launch duration)')
     ap.add_argument('--no-config-legs', action='store_true',
