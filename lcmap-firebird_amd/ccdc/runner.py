@@ -169,22 +169,30 @@ class ParquetSink(object):
     Parquet encoding costs ~0.7 s of one core per C3 chip (the pixel table's n_pix x n_obs mask
     entries), far more than its detection: ``threads`` > 0 writes on a pool of
     that many threads (pyarrow encodes without the GIL) from copies of the chip's arrays, so
-    the runner's workers hand a chip over and go back to the device.  ``flush()`` waits for the
-    writes and raises the first write error; the tile driver calls it before it returns.
+    the runner's workers hand a chip over and go back to the device -- at most ``max_pending``
+    chips (default 2 x threads) wait for a writer, beyond that the handing worker blocks, so the
+    copies held for the pool stay bounded when the writers are slower than the device (they are:
+    ~12 chips/s against ~330).  ``flush()`` waits for the writes and raises the first write error;
+    the tile driver calls it before it returns.
     ``options``: pyarrow.parquet.write_table options for every file.  Measured on one MI355X box
     (16 CPUs, `tools/parquet_tile.py`, 96 chips): 7.6 chips/s inline, 10.9 / 11.9 with 8 / 14
     writer threads -- the box's CPUs, not the device, bound a tile written this way."""
 
-    def __init__(self, directory, threads=0, **options):
+    def __init__(self, directory, threads=0, max_pending=None, **options):
         self.directory = directory
         self.options = options  # pyarrow.parquet.write_table options (ccdc.sink.write_parquet)
         self.summary = SummarySink()
         self._pool = None
         self._pending = []
         self._lock = threading.Lock()
+        self._slots = None
         if int(threads) > 0:
             from concurrent.futures import ThreadPoolExecutor
             self._pool = ThreadPoolExecutor(int(threads), thread_name_prefix='ccd-parquet')
+            n = int(max_pending) if max_pending is not None else 2 * int(threads)
+            if n < 1:
+                raise ValueError('max_pending must be >= 1, got %d' % n)
+            self._slots = threading.BoundedSemaphore(n)
 
     def _write(self, cx, cy, dates, row_offsets, rows, mask_bits):
         from ccdc import sink
@@ -198,8 +206,14 @@ class ParquetSink(object):
             self._write(cx, cy, dates, row_offsets, rows, mask_bits)
         else:
             # the runner's arrays are views of reused landing buffers: copies go to the pool
-            f = self._pool.submit(self._write, cx, cy, np.array(dates), np.array(row_offsets), np.array(rows),
-                                  np.array(mask_bits))
+            self._slots.acquire()  # backpressure: at most max_pending chips queued or being written
+            try:
+                f = self._pool.submit(self._write, cx, cy, np.array(dates), np.array(row_offsets), np.array(rows),
+                                      np.array(mask_bits))
+            except BaseException:
+                self._slots.release()
+                raise
+            f.add_done_callback(lambda _f: self._slots.release())
             with self._lock:
                 self._pending.append(f)
         self.summary(pos, cx, cy, dates, row_offsets, rows, mask_bits)

@@ -376,3 +376,50 @@ def test_parquet_sink_write_error_reaches_the_caller(tmp_path):
         runner.changedetection(tile(), source, contexts=1, batch_chips=2, number=2, sink=ps,
                                context_factory=lambda dev: OracleContext(dev, threads=2))
     ps.close()  # (the failed write was raised above; nothing left pending)
+
+
+def test_parquet_sink_pool_bounds_the_chips_waiting_for_a_writer(tmp_path):
+    """ParquetSink(threads, max_pending): with writers far slower than the hand-over (as Parquet
+    encoding is against the device), at most max_pending chips' copies are queued or being
+    written; the handing thread blocks instead of queueing every chip of the tile."""
+    import threading
+    import time
+    from ccdc import runner
+    ps = runner.ParquetSink(str(tmp_path), threads=2, max_pending=3)
+    lock = threading.Lock()
+    state = {'live': 0, 'peak': 0, 'done': 0}
+
+    def slow_write(*args):
+        with lock:
+            state['live'] += 1
+        time.sleep(0.02)
+        with lock:
+            state['live'] -= 1
+            state['done'] += 1
+
+    ps._write = slow_write
+    queued = []
+    orig_submit = ps._pool.submit
+
+    def counting_submit(*a, **k):
+        f = orig_submit(*a, **k)
+        with lock:
+            queued.append(f)
+            state['peak'] = max(state['peak'], sum(1 for q in queued if not q.done()))
+        return f
+
+    ps._pool.submit = counting_submit
+    seen = []
+    ps.summary = lambda pos, *a: seen.append(pos)  # (the chip record is not under test here)
+    d = np.arange(5, dtype=np.int64)
+    off = np.array([0, 1], dtype=np.int64)
+    rows = np.zeros(1, dtype=np.int32)
+    mb = np.zeros((1, 1), dtype=np.uint64)
+    for pos in range(12):
+        ps(pos, 0, 0, d, off, rows, mb)
+    ps.close()
+    assert state['done'] == 12 and state['live'] == 0
+    assert state['peak'] <= 3, state
+    assert seen == list(range(12))
+    with pytest.raises(ValueError):
+        runner.ParquetSink(str(tmp_path), threads=1, max_pending=0)
