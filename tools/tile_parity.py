@@ -133,6 +133,8 @@ def main():
     ap.add_argument('--sample', type=int, default=100)
     ap.add_argument('--config', type=int, default=3)
     ap.add_argument('--batch', type=int, default=8)
+    ap.add_argument('--offset', type=int, default=0,
+                    help='generator chip of position 0 (2500: the next tile\'s chips, other seeds and cadences)')
     ap.add_argument('--oracle-threads', type=int, default=int(os.environ.get('OMP_NUM_THREADS', '16') or 16) - 1)
     ap.add_argument('--out', default=os.path.join(ROOT, 'gpurun_out', 'tile_parity.json'))
     ap.add_argument('--encode', choices=('unread', 'lossless', 'none'), default='unread', help='upload of the chips (the runner\'s default: unread)')
@@ -156,7 +158,8 @@ def main():
                 pass
         synth.TileSource._gen = lambda self: HostGen()
         factory = lambda dev: rows_util.OracleContext(dev, threads=4)
-    src = ParitySource(cfg, pool, args.sample, batch_chips=args.batch, pinned=not args.cpu_dry_run)
+    src = ParitySource(cfg, pool, args.sample, batch_chips=args.batch, pinned=not args.cpu_dry_run,
+                       chip_of=lambda pos: int(pos) + args.offset)
     sink = SampleSink(args.sample)
     xys = [(-1815585 + 3000 * (c // 50), 1064805 - 3000 * (c % 50)) for c in range(args.chips)]
     t = time.perf_counter()
@@ -190,8 +193,9 @@ def main():
     for c in res['chips']:
         mix[c['n_obs']] = mix.get(c['n_obs'], 0) + 1
     out = {
-        'what': 'tile parity: ccdc.runner.changedetection over %d distinct generated chips (config %d), a stratified '
-                'sample of %d pixels per chip vs the C restatement oracle' % (args.chips, args.config, args.sample),
+        'what': 'tile parity: ccdc.runner.changedetection over %d distinct generated chips (config %d, generator chips '
+                '%d ..), a stratified sample of %d pixels per chip vs the C restatement oracle' % (
+                    args.chips, args.config, args.offset, args.sample),
         'chips': len(res['chips']), 'distinct_chip_ids': len(set(src.futures)), 'n_obs_mix': mix,
         'tile_pixels': sum(c['n_pix'] for c in res['chips']), 'tile_rows': sum(c['rows'] for c in res['chips']),
         'sampled_pixels': tot['pixels'], 'sampled_rows': tot['segments'],
