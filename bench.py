@@ -709,11 +709,11 @@ def tile_leg(args, cfg, rank, world, device, dist, split=False):
         dist.barrier()
     el = max_over_ranks(time.perf_counter() - t, dist)
     thread_cpu = tcpu.stop()
+    cg1 = _cgroup_cpu()  # (before the parity checker: its oracle threads are not the tile's CPU)
     parity = None
     if sample_sink[0] is not None:
         parity = tile_parity_sample(sample_sink[0], src, cfg, mode, dist)
     gen_s = src.generate_seconds - gen0
-    cg1 = _cgroup_cpu()
     cg = None
     if cg0 and cg1:
         cg = {k.replace('_usec', '_s'): round((cg1[k] - cg0[k]) / 1e6, 3) for k in cg0 if k in cg1 and k.endswith('usec')}
